@@ -1,0 +1,141 @@
+"""ctypes binding of libacm.so (the C-ABI declared in include/acm.h).
+
+The product path runs only through this library: there is no CPU fallback.
+If libacm.so is missing, importing the package raises -- build it with
+``python -c "import __graft_entry__ as g; g.build()"`` (or ``make -C
+apex-camera-models_amd``).
+
+torch is imported first on purpose: torch ships its own libamdhip64.so.7 and
+libacm.so links the same SONAME, so loading torch first makes both share ONE
+HIP runtime (device pointers and streams from torch are then valid here).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module doc)
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libacm.so")
+
+# model ids / codes (include/acm.h)
+PINHOLE, RADTAN, KANNALA_BRANDT, DOUBLE_SPHERE, UCM, EUCM, FOV = range(7)
+LAYOUT_AOS, LAYOUT_SOA = 0, 1
+INVALID_SKIP, INVALID_SENTINEL = 0, 1
+MAX_PARAMS = 9
+
+ACM_SUCCESS = 0
+ERR_INVALID_MODEL = -1
+ERR_INVALID_PARAMS = -2
+ERR_INVALID_ARGUMENT = -3
+ERR_HIP = -4
+ERR_WORKSPACE_TOO_SMALL = -5
+
+
+class AcmCamera(ctypes.Structure):
+    _fields_ = [
+        ("model", ctypes.c_int32),
+        ("width", ctypes.c_uint32),
+        ("height", ctypes.c_uint32),
+        ("num_params", ctypes.c_uint32),
+        ("params", ctypes.c_double * MAX_PARAMS),
+    ]
+
+
+EXPORTED_SYMBOLS = (
+    "acm_num_params",
+    "acm_camera_init",
+    "acm_validate_params",
+    "acm_project",
+    "acm_unproject",
+    "acm_residual_jacobian",
+    "acm_normal_equations_workspace_size",
+    "acm_normal_equations",
+    "acm_reprojection_stats_workspace_size",
+    "acm_reprojection_stats",
+    "acm_median_workspace_size",
+    "acm_median_valid",
+    "acm_sample_points_grid",
+    "acm_sample_points_workspace_size",
+    "acm_sample_points",
+    "acm_last_hip_error",
+    "acm_last_error",
+    "acm_version",
+)
+
+_lib = None
+
+
+class AcmError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libacm error {code}: {msg}")
+        self.code = code
+
+
+def load():
+    """Load libacm.so and declare every C-ABI signature (fails loudly)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libacm.so not found at {LIB_PATH}: the HIP extension is not built "
+            "(run __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    cam_p = ctypes.POINTER(AcmCamera)
+    vp = ctypes.c_void_p
+    sz = ctypes.c_size_t
+    i = ctypes.c_int
+    L.acm_num_params.argtypes = [i]
+    L.acm_num_params.restype = i
+    L.acm_camera_init.argtypes = [cam_p, i, ctypes.POINTER(ctypes.c_double), sz,
+                                  ctypes.c_uint32, ctypes.c_uint32]
+    L.acm_camera_init.restype = i
+    L.acm_validate_params.argtypes = [cam_p]
+    L.acm_validate_params.restype = i
+    L.acm_project.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp]
+    L.acm_project.restype = i
+    L.acm_unproject.argtypes = [cam_p, sz, vp, vp, i, vp, vp]
+    L.acm_unproject.restype = i
+    L.acm_residual_jacobian.argtypes = [cam_p, sz, vp, i, vp, i, vp, vp, vp, vp]
+    L.acm_residual_jacobian.restype = i
+    L.acm_normal_equations_workspace_size.argtypes = [i, sz]
+    L.acm_normal_equations_workspace_size.restype = sz
+    L.acm_normal_equations.argtypes = [cam_p, sz, vp, i, vp, i, vp, vp, sz, vp]
+    L.acm_normal_equations.restype = i
+    L.acm_reprojection_stats_workspace_size.argtypes = [sz]
+    L.acm_reprojection_stats_workspace_size.restype = sz
+    L.acm_reprojection_stats.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp, sz, vp]
+    L.acm_reprojection_stats.restype = i
+    L.acm_sample_points_grid.argtypes = [ctypes.c_uint32, ctypes.c_uint32, sz,
+                                         ctypes.POINTER(ctypes.c_uint32),
+                                         ctypes.POINTER(ctypes.c_uint32)]
+    L.acm_sample_points_grid.restype = i
+    L.acm_sample_points_workspace_size.argtypes = [cam_p, sz]
+    L.acm_sample_points_workspace_size.restype = sz
+    L.acm_sample_points.argtypes = [cam_p, sz, vp, vp, vp, vp, sz, vp]
+    L.acm_sample_points.restype = i
+    L.acm_median_workspace_size.argtypes = [sz]
+    L.acm_median_workspace_size.restype = sz
+    L.acm_median_valid.argtypes = [sz, vp, vp, ctypes.c_uint64, vp, vp, sz, vp]
+    L.acm_median_valid.restype = i
+    L.acm_last_hip_error.argtypes = []
+    L.acm_last_hip_error.restype = i
+    L.acm_last_error.argtypes = []
+    L.acm_last_error.restype = ctypes.c_char_p
+    L.acm_version.argtypes = []
+    L.acm_version.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        msg = load().acm_last_error().decode(errors="replace")
+        raise AcmError(rc, msg)
+    return rc
+
+
+def last_error() -> str:
+    return load().acm_last_error().decode(errors="replace")

@@ -1,0 +1,102 @@
+"""Mirror of the reference's hot-path utilities (src/util/).
+
+`sample_points` (point_sampling.rs:46-120) and `compute_reprojection_error`
+(error_metrics.rs:62-121), both evaluated by libacm.so kernels on device
+tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .camera import CameraModel, _as_device_f64, _stream_handle
+
+
+class UtilError(Exception):
+    pass
+
+
+class ZeroProjectionPoints(UtilError):
+    def __init__(self):
+        super().__init__("Zero projection points")
+
+
+@dataclass
+class ProjectionError:
+    rmse: float
+    min: float
+    max: float
+    mean: float
+    stddev: float
+    median: float
+    n_valid: int = 0
+
+
+def sample_points(camera_model: CameraModel, n: int):
+    """Grid of ~n pixel-cell centres, unprojected; keeps Ok && z > 0, in order.
+
+    Returns (points_2d (M,2), points_3d (M,3)) float64 device tensors.
+    """
+    L = _lib.load()
+    cam = camera_model.acm_camera()
+    ncx, ncy = ctypes.c_uint32(), ctypes.c_uint32()
+    _lib.check(L.acm_sample_points_grid(cam.width, cam.height, n, ctypes.byref(ncx),
+                                        ctypes.byref(ncy)))
+    cap = ncx.value * ncy.value
+    dev = torch.device("cuda")
+    uv = torch.empty((cap, 2), dtype=torch.float64, device=dev)
+    xyz = torch.empty((cap, 3), dtype=torch.float64, device=dev)
+    counts = torch.zeros((2,), dtype=torch.int64, device=dev)
+    ws_bytes = L.acm_sample_points_workspace_size(ctypes.byref(cam), n)
+    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=dev)
+    _lib.check(L.acm_sample_points(ctypes.byref(cam), n, uv.data_ptr(), xyz.data_ptr(),
+                                   counts.data_ptr(), ws.data_ptr(), ws_bytes,
+                                   _stream_handle()))
+    m = int(counts[0].item())
+    return uv[:m], xyz[:m]
+
+
+def reprojection_stats(camera_model: CameraModel, points3d, points2d, errors=None):
+    """Device result [rmse, min, max, mean, stddev, n_valid, sum, sumsq]."""
+    L = _lib.load()
+    p3 = _as_device_f64(points3d, 3)
+    p2 = _as_device_f64(points2d, 2)
+    n = p3.shape[0]
+    if p2.shape[0] != n:
+        raise ValueError("points3d and points2d must have the same number of columns")
+    ws_bytes = L.acm_reprojection_stats_workspace_size(n)
+    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=p3.device)
+    out = torch.empty((8,), dtype=torch.float64, device=p3.device)
+    cam = camera_model.acm_camera()
+    _lib.check(L.acm_reprojection_stats(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
+                                        p2.data_ptr(), out.data_ptr(),
+                                        errors.data_ptr() if errors is not None else None,
+                                        ws.data_ptr(), ws_bytes, _stream_handle()))
+    return out
+
+
+def compute_reprojection_error(camera_model: CameraModel, points3d, points2d) -> ProjectionError:
+    """error_metrics.rs:62-121 (median: see reprojection_median)."""
+    p3 = _as_device_f64(points3d, 3)
+    errors = torch.empty((p3.shape[0],), dtype=torch.float64, device=p3.device)
+    out = reprojection_stats(camera_model, p3, points2d, errors).cpu().tolist()
+    n_valid = int(out[5])
+    if n_valid == 0:
+        raise ZeroProjectionPoints()
+    median = reprojection_median(errors, n_valid)
+    return ProjectionError(rmse=out[0], min=out[1], max=out[2], mean=out[3], stddev=out[4],
+                           median=median, n_valid=n_valid)
+
+
+def reprojection_median(errors: torch.Tensor, n_valid: int) -> float:
+    """Median of the valid (non-NaN) errors (error_metrics.rs:104-111)."""
+    L = _lib.load()
+    out = torch.empty((1,), dtype=torch.float64, device=errors.device)
+    ws_bytes = L.acm_median_workspace_size(errors.numel())
+    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=errors.device)
+    _lib.check(L.acm_median_valid(errors.numel(), errors.data_ptr(), None, n_valid, out.data_ptr(),
+                                  ws.data_ptr(), ws_bytes, _stream_handle()))
+    return float(out.item())

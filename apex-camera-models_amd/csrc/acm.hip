@@ -1,0 +1,923 @@
+// acm.hip -- MI355X (gfx950) kernels and the C-ABI of libacm.so.
+//
+// The hot path of the reference (per-point CameraModel::project/unproject and
+// the apex-solver *CameraParamsFactor linearisation, see include/acm.h) is a
+// pure streaming map: every point is independent and touches 41-185 bytes of
+// HBM for ~100-400 f64 operations.  It is bound by HBM bandwidth, so the
+// kernels are built around the memory system, not MFMA:
+//   * one point per lane, 256-lane workgroups, one launch covers the batch
+//     (10M points -> 39k workgroups, far more than the 256 CUs x 8 slots);
+//   * inputs read once, outputs written once, every store 16 B per lane and
+//     contiguous across the wave (uv pairs, the (du,dv) pair of each column
+//     of the 2N x P column-major Jacobian), status bytes contiguous;
+//   * camera parameters arrive by value in the kernel arguments -> SGPRs;
+//   * the reductions (normal equations, residual norms) keep per-lane sums
+//     in registers, reduce with wave64 shuffles, then across the 4 waves of
+//     a workgroup in LDS, and finish with a fixed-order second pass, so the
+//     result is bit-reproducible run to run.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "acm.h"
+#include "camera_models.hpp"
+
+namespace acm {
+
+static thread_local std::string g_last_error;
+static thread_local int g_last_hip_error = 0;
+
+static int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+static int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_last_hip_error = (int)e;
+        return fail(ACM_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    }
+    return ACM_SUCCESS;
+}
+
+template <template <class> class M>
+struct Tag {
+    template <class T>
+    using type = M<T>;
+};
+
+template <class F>
+static int dispatch_model(int model, F&& f) {
+    switch (model) {
+    case ACM_PINHOLE: return f(Tag<Pinhole>{});
+    case ACM_RADTAN: return f(Tag<RadTan>{});
+    case ACM_KANNALA_BRANDT: return f(Tag<KannalaBrandt>{});
+    case ACM_DOUBLE_SPHERE: return f(Tag<DoubleSphere>{});
+    case ACM_UCM: return f(Tag<Ucm>{});
+    case ACM_EUCM: return f(Tag<Eucm>{});
+    case ACM_FOV: return f(Tag<Fov>{});
+    default: return fail(ACM_ERR_INVALID_MODEL, "unknown camera model id");
+    }
+}
+
+template <class T>
+__device__ __forceinline__ Cam<T> make_cam(const acm_camera& c) {
+    Cam<T> k;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) k.p[i] = (T)c.params[i];
+    k.w = (T)(double)c.width;
+    k.h = (T)(double)c.height;
+    k.wi = c.width;
+    k.hi = c.height;
+    return k;
+}
+
+template <int LAYOUT>
+__device__ __forceinline__ void load_point(const double* __restrict__ pts, size_t n, size_t i,
+                                           double& x, double& y, double& z) {
+    if (LAYOUT == ACM_LAYOUT_AOS) {
+        x = pts[3 * i];
+        y = pts[3 * i + 1];
+        z = pts[3 * i + 2];
+    } else {
+        x = pts[i];
+        y = pts[n + i];
+        z = pts[2 * n + i];
+    }
+}
+
+constexpr int kBlock = 256;
+
+// ------------------------------------------------------------ project (+J)
+template <class TagT, int LAYOUT, bool WJ>
+__global__ __launch_bounds__(kBlock) void k_project(acm_camera cam, size_t n,
+                                                    const double* __restrict__ pts,
+                                                    double* __restrict__ uv,
+                                                    uint8_t* __restrict__ status,
+                                                    double* __restrict__ jac) {
+    using M = typename TagT::template type<double>;
+    constexpr int P = M::P;
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const Cam<double> c = make_cam<double>(cam);
+    double x, y, z;
+    load_point<LAYOUT>(pts, n, i, x, y, z);
+    double u, v, ju[P], jv[P];
+    const uint8_t st = M::template project<WJ>(c, x, y, z, u, v, ju, jv);
+    const bool ok = st == ST_OK;
+    *reinterpret_cast<double2*>(uv + 2 * i) =
+        ok ? make_double2(u, v) : make_double2(__builtin_nan(""), __builtin_nan(""));
+    status[i] = st;
+    if (WJ) {
+        const size_t col = 2 * n;
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+            *reinterpret_cast<double2*>(jac + p * col + 2 * i) =
+                ok ? make_double2(ju[p], jv[p]) : make_double2(0.0, 0.0);
+    }
+}
+
+// --------------------------------------------------------------- unproject
+template <class TagT, int LAYOUT>
+__global__ __launch_bounds__(kBlock) void k_unproject(acm_camera cam, size_t n,
+                                                      const double* __restrict__ uv,
+                                                      double* __restrict__ rays,
+                                                      uint8_t* __restrict__ status) {
+    using M = typename TagT::template type<double>;
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const Cam<double> c = make_cam<double>(cam);
+    const double2 q = *reinterpret_cast<const double2*>(uv + 2 * i);
+    double X, Y, Z;
+    const uint8_t st = M::unproject(c, q.x, q.y, X, Y, Z);
+    if (st != ST_OK) X = Y = Z = __builtin_nan("");
+    if (LAYOUT == ACM_LAYOUT_AOS) {
+        rays[3 * i] = X;
+        rays[3 * i + 1] = Y;
+        rays[3 * i + 2] = Z;
+    } else {
+        rays[i] = X;
+        rays[n + i] = Y;
+        rays[2 * n + i] = Z;
+    }
+    status[i] = st;
+}
+
+// -------------------------------------------------- residual + Jacobian
+template <class TagT, int LAYOUT, bool WJ>
+__global__ __launch_bounds__(kBlock) void k_residual(acm_camera cam, size_t n,
+                                                     const double* __restrict__ pts,
+                                                     const double* __restrict__ obs,
+                                                     int policy, double* __restrict__ res,
+                                                     double* __restrict__ jac,
+                                                     uint8_t* __restrict__ status) {
+    using M = typename TagT::template type<double>;
+    constexpr int P = M::P;
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const Cam<double> c = make_cam<double>(cam);
+    double x, y, z;
+    load_point<LAYOUT>(pts, n, i, x, y, z);
+    const double2 o = *reinterpret_cast<const double2*>(obs + 2 * i);
+    double u, v, ju[P], jv[P];
+    const uint8_t st = M::template project<WJ>(c, x, y, z, u, v, ju, jv);
+    const bool ok = st == ST_OK;
+    const double sent = policy == ACM_INVALID_SENTINEL ? 1e6 : 0.0;
+    *reinterpret_cast<double2*>(res + 2 * i) =
+        ok ? make_double2(u - o.x, v - o.y) : make_double2(sent, sent);
+    if (status) status[i] = st;
+    if (WJ) {
+        const size_t col = 2 * n;
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+            *reinterpret_cast<double2*>(jac + p * col + 2 * i) =
+                ok ? make_double2(ju[p], jv[p]) : make_double2(0.0, 0.0);
+    }
+}
+
+// -------------------------------------------------- wave / block reduction
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Reduce K per-lane values across the workgroup into out[0..K) (LDS staged).
+template <int K>
+__device__ __forceinline__ void block_sum_store(const double (&acc)[K], double* __restrict__ out) {
+    __shared__ double sm[kBlock / 64][K];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double s = wave_sum(acc[k]);
+        if (lane == 0) sm[wid][k] = s;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < K; k += kBlock) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) s += sm[w][k];
+        out[k] = s;
+    }
+}
+
+// Second pass: column k of `parts` ([nb][K]) summed in a fixed order by one
+// workgroup per k (deterministic).
+__global__ __launch_bounds__(kBlock) void k_sum_columns(const double* __restrict__ parts, int nb,
+                                                        int K, double* __restrict__ out) {
+    const int k = blockIdx.x;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < nb; b += kBlock) s += parts[(size_t)b * K + k];
+    __shared__ double sm[kBlock / 64];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < kBlock / 64; ++w) t += sm[w];
+        out[k] = t;
+    }
+}
+
+// ---------------------------------------------------- normal equations
+// acc layout: [upper triangle of JtJ (P(P+1)/2) | Jtr (P) | sum r.r | n_valid]
+template <int P>
+struct NE {
+    static constexpr int T = P * (P + 1) / 2;
+    static constexpr int K = T + P + 2;
+};
+
+constexpr int kNeMaxBlocks = 1024;
+
+static int ne_blocks(size_t n) {
+    size_t b = (n + kBlock - 1) / kBlock;
+    if (b > (size_t)kNeMaxBlocks) b = kNeMaxBlocks;
+    if (b == 0) b = 1;
+    return (int)b;
+}
+
+template <class TagT, int LAYOUT>
+__global__ __launch_bounds__(kBlock) void k_normal_eq(acm_camera cam, size_t n,
+                                                      const double* __restrict__ pts,
+                                                      const double* __restrict__ obs, int policy,
+                                                      double* __restrict__ parts) {
+    using M = typename TagT::template type<double>;
+    constexpr int P = M::P;
+    constexpr int K = NE<P>::K;
+    const Cam<double> c = make_cam<double>(cam);
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        double x, y, z;
+        load_point<LAYOUT>(pts, n, i, x, y, z);
+        const double2 o = *reinterpret_cast<const double2*>(obs + 2 * i);
+        double u, v, ju[P], jv[P];
+        const uint8_t st = M::template project<true>(c, x, y, z, u, v, ju, jv);
+        if (st == ST_OK) {
+            const double r0 = u - o.x, r1 = v - o.y;
+            int t = 0;
+#pragma unroll
+            for (int a = 0; a < P; ++a) {
+#pragma unroll
+                for (int b = a; b < P; ++b) acc[t++] += ju[a] * ju[b] + jv[a] * jv[b];
+            }
+#pragma unroll
+            for (int a = 0; a < P; ++a) acc[NE<P>::T + a] += ju[a] * r0 + jv[a] * r1;
+            acc[K - 2] += r0 * r0 + r1 * r1;
+            acc[K - 1] += 1.0;
+        } else {
+            acc[K - 2] += sent2;
+        }
+    }
+    block_sum_store<K>(acc, parts + (size_t)blockIdx.x * K);
+}
+
+// expand [tri | Jtr | rr | nv] -> [JtJ full (P*P) | Jtr | 0.5*rr | nv]
+__global__ void k_ne_expand(const double* __restrict__ sums, int P, double* __restrict__ out) {
+    const int T = P * (P + 1) / 2;
+    if (threadIdx.x != 0) return;
+    int t = 0;
+    for (int a = 0; a < P; ++a)
+        for (int b = a; b < P; ++b) {
+            out[a * P + b] = sums[t];
+            out[b * P + a] = sums[t];
+            ++t;
+        }
+    for (int a = 0; a < P; ++a) out[P * P + a] = sums[T + a];
+    out[P * P + P] = 0.5 * sums[T + P];
+    out[P * P + P + 1] = sums[T + P + 1];
+}
+
+// ----------------------------------------------------- reprojection stats
+// pass 1: e_i = ||proj(p_i) - uv_i|| (NaN if the projection fails);
+// per-block [sum e, sum e^2, min, max, count]
+template <class TagT, int LAYOUT>
+__global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t n,
+                                                         const double* __restrict__ pts,
+                                                         const double* __restrict__ obs,
+                                                         double* __restrict__ errs,
+                                                         double* __restrict__ parts) {
+    using M = typename TagT::template type<double>;
+    const Cam<double> c = make_cam<double>(cam);
+    double s = 0.0, ss = 0.0, mn = INFINITY, mx = -INFINITY, cnt = 0.0;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        double x, y, z;
+        load_point<LAYOUT>(pts, n, i, x, y, z);
+        const double2 o = *reinterpret_cast<const double2*>(obs + 2 * i);
+        double u, v;
+        const uint8_t st = M::template project<false>(c, x, y, z, u, v, nullptr, nullptr);
+        double e = __builtin_nan("");
+        if (st == ST_OK) {
+            const double du = u - o.x, dv = v - o.y;
+            e = sqrt(du * du + dv * dv);
+            s += e;
+            ss += e * e;
+            mn = fmin(mn, e);
+            mx = fmax(mx, e);
+            cnt += 1.0;
+        }
+        errs[i] = e;
+    }
+    // sums
+    __shared__ double sm[kBlock / 64][5];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    s = wave_sum(s);
+    ss = wave_sum(ss);
+    cnt = wave_sum(cnt);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        mn = fmin(mn, __shfl_xor(mn, off, 64));
+        mx = fmax(mx, __shfl_xor(mx, off, 64));
+    }
+    if (lane == 0) {
+        sm[wid][0] = s; sm[wid][1] = ss; sm[wid][2] = mn; sm[wid][3] = mx; sm[wid][4] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0, b = 0, m0 = INFINITY, m1 = -INFINITY, k = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            a += sm[w][0]; b += sm[w][1]; m0 = fmin(m0, sm[w][2]); m1 = fmax(m1, sm[w][3]);
+            k += sm[w][4];
+        }
+        double* o = parts + (size_t)blockIdx.x * 5;
+        o[0] = a; o[1] = b; o[2] = m0; o[3] = m1; o[4] = k;
+    }
+}
+
+// fixed-order finish of pass 1: tot = [sum, sumsq, min, max, count]
+__global__ __launch_bounds__(kBlock) void k_reproj_finish1(const double* __restrict__ parts,
+                                                           int nb, double* __restrict__ tot) {
+    double s = 0, ss = 0, mn = INFINITY, mx = -INFINITY, cnt = 0;
+    for (int b = threadIdx.x; b < nb; b += kBlock) {
+        const double* p = parts + (size_t)b * 5;
+        s += p[0]; ss += p[1]; mn = fmin(mn, p[2]); mx = fmax(mx, p[3]); cnt += p[4];
+    }
+    __shared__ double sm[kBlock / 64][5];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    s = wave_sum(s);
+    ss = wave_sum(ss);
+    cnt = wave_sum(cnt);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        mn = fmin(mn, __shfl_xor(mn, off, 64));
+        mx = fmax(mx, __shfl_xor(mx, off, 64));
+    }
+    if (lane == 0) {
+        sm[wid][0] = s; sm[wid][1] = ss; sm[wid][2] = mn; sm[wid][3] = mx; sm[wid][4] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0, b = 0, m0 = INFINITY, m1 = -INFINITY, k = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            a += sm[w][0]; b += sm[w][1]; m0 = fmin(m0, sm[w][2]); m1 = fmax(m1, sm[w][3]);
+            k += sm[w][4];
+        }
+        tot[0] = a; tot[1] = b; tot[2] = m0; tot[3] = m1; tot[4] = k;
+    }
+}
+
+// pass 2: per-block sum (e - mean)^2 over valid errors (error_metrics.rs:92)
+__global__ __launch_bounds__(kBlock) void k_reproj_pass2(size_t n, const double* __restrict__ errs,
+                                                         const double* __restrict__ tot,
+                                                         double* __restrict__ parts) {
+    const double mean = tot[0] / tot[4];
+    double acc[1] = {0.0};
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const double e = errs[i];
+        if (e == e) {
+            const double d = e - mean;
+            acc[0] += d * d;
+        }
+    }
+    block_sum_store<1>(acc, parts + blockIdx.x);
+}
+
+// result = [rmse, min, max, mean, stddev, n_valid, sum, sumsq]
+__global__ void k_reproj_final(const double* __restrict__ tot, const double* __restrict__ var_sum,
+                               double* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const double nn = tot[4];
+    const double mean = tot[0] / nn;
+    out[0] = sqrt(tot[1] / nn);
+    out[1] = tot[2];
+    out[2] = tot[3];
+    out[3] = mean;
+    out[4] = sqrt(var_sum[0] / nn);
+    out[5] = nn;
+    out[6] = tot[0];
+    out[7] = tot[1];
+}
+
+// ------------------------------------------------------------ sample_points
+// point_sampling.rs:56-103.  Cell c = i*ncx + j (row-major like the
+// reference's nested loop).  Two passes with the unprojection recomputed in
+// the second (cheaper than a 40 B/cell scratch round trip through HBM):
+//   1. per-workgroup keep counts, 2. exclusive scan of the counts (one
+//   workgroup), 3. keep -> rank inside the workgroup (wave ballot + LDS
+//   prefix over the 4 waves) -> ordered scatter.
+struct Grid {
+    uint32_t ncx, ncy;
+    double cw, ch;
+};
+
+template <class TagT>
+__device__ __forceinline__ bool sample_cell(const Cam<double>& c, const Grid& g, size_t cell,
+                                            double& u, double& v, double& X, double& Y,
+                                            double& Z) {
+    using M = typename TagT::template type<double>;
+    const uint32_t i = (uint32_t)(cell / g.ncx), j = (uint32_t)(cell % g.ncx);
+    u = ((double)j + 0.5) * g.cw;  // :69
+    v = ((double)i + 0.5) * g.ch;  // :70
+    const uint8_t st = M::unproject(c, u, v, X, Y, Z);
+    return st == ST_OK && Z > 0.0;  // :91-94
+}
+
+template <class TagT>
+__global__ __launch_bounds__(kBlock) void k_sample_count(acm_camera cam, Grid g, size_t cells,
+                                                         uint64_t* __restrict__ counts) {
+    const Cam<double> c = make_cam<double>(cam);
+    const size_t cell = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    bool keep = false;
+    if (cell < cells) {
+        double u, v, X, Y, Z;
+        keep = sample_cell<TagT>(c, g, cell, u, v, X, Y, Z);
+    }
+    const uint64_t m = __ballot(keep);
+    __shared__ uint32_t sm[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += sm[w];
+        counts[blockIdx.x] = t;
+    }
+}
+
+// exclusive scan of nb block counts by one workgroup of 1024 lanes
+__global__ __launch_bounds__(1024) void k_scan_counts(const uint64_t* __restrict__ counts,
+                                                      size_t nb, uint64_t* __restrict__ offsets,
+                                                      uint64_t* __restrict__ out_counts,
+                                                      uint64_t cells) {
+    const size_t per = (nb + 1023) / 1024;
+    const size_t b0 = (size_t)threadIdx.x * per;
+    uint64_t s = 0;
+    for (size_t b = b0; b < b0 + per && b < nb; ++b) s += counts[b];
+    __shared__ uint64_t sm[1024];
+    sm[threadIdx.x] = s;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over the 1024 thread sums
+    for (int off = 1; off < 1024; off <<= 1) {
+        uint64_t t = threadIdx.x >= (unsigned)off ? sm[threadIdx.x - off] : 0;
+        __syncthreads();
+        sm[threadIdx.x] += t;
+        __syncthreads();
+    }
+    uint64_t run = sm[threadIdx.x] - s;  // exclusive prefix of this thread's run
+    for (size_t b = b0; b < b0 + per && b < nb; ++b) {
+        offsets[b] = run;
+        run += counts[b];
+    }
+    if (threadIdx.x == 1023) {
+        out_counts[0] = sm[1023];
+        out_counts[1] = cells;
+    }
+}
+
+template <class TagT>
+__global__ __launch_bounds__(kBlock) void k_sample_write(acm_camera cam, Grid g, size_t cells,
+                                                         const uint64_t* __restrict__ offsets,
+                                                         double* __restrict__ uv_out,
+                                                         double* __restrict__ xyz_out) {
+    const Cam<double> c = make_cam<double>(cam);
+    const size_t cell = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    bool keep = false;
+    double u = 0, v = 0, X = 0, Y = 0, Z = 0;
+    if (cell < cells) keep = sample_cell<TagT>(c, g, cell, u, v, X, Y, Z);
+    const uint64_t m = __ballot(keep);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ uint32_t sm[kBlock / 64];
+    if (lane == 0) sm[wid] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint64_t base = offsets[blockIdx.x];
+    for (int w = 0; w < wid; ++w) base += sm[w];
+    const uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    if (keep) {
+        const size_t k = base + (uint64_t)__popcll(below);
+        *reinterpret_cast<double2*>(uv_out + 2 * k) = make_double2(u, v);
+        xyz_out[3 * k] = X;
+        xyz_out[3 * k + 1] = Y;
+        xyz_out[3 * k + 2] = Z;
+    }
+}
+
+// ----------------------------------------------------------------- median
+// Exact median of the valid (non-NaN, >= 0) errors, error_metrics.rs:104-111,
+// without a full sort: MSB-first radix select on the f64 bit patterns (for
+// non-negative doubles the unsigned bit order is the numeric order; the NaN
+// markers 0x7ff8.. sort above +inf so they never reach a rank < n_valid).
+// 8 histogram passes of 8 bits per selected rank; state lives on device.
+struct SelState {
+    unsigned long long prefix, mask, k;
+};
+
+__global__ __launch_bounds__(kBlock) void k_sel_hist(size_t n, const double* __restrict__ vals,
+                                                     const SelState* __restrict__ st, int shift,
+                                                     unsigned long long* __restrict__ hist) {
+    __shared__ unsigned int h[256];
+    h[threadIdx.x] = 0;  // kBlock == 256
+    __syncthreads();
+    const unsigned long long prefix = st->prefix, mask = st->mask;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const unsigned long long b = (unsigned long long)__double_as_longlong(vals[i]);
+        if ((b & mask) == prefix) atomicAdd(&h[(b >> shift) & 0xFFull], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+__global__ void k_sel_pick(SelState* __restrict__ st, int shift,
+                           unsigned long long* __restrict__ hist) {
+    if (threadIdx.x != 0) return;
+    unsigned long long k = st->k, run = 0;
+    int b = 0;
+    for (; b < 256; ++b) {
+        if (run + hist[b] > k) break;
+        run += hist[b];
+    }
+    if (b == 256) b = 255;
+    st->k = k - run;
+    st->prefix |= (unsigned long long)b << shift;
+    st->mask |= 0xFFull << shift;
+    for (int j = 0; j < 256; ++j) hist[j] = 0;
+}
+
+__global__ void k_sel_init(SelState* __restrict__ st, const double* __restrict__ nvalid_src,
+                           unsigned long long nvalid_fixed, int which,
+                           unsigned long long* __restrict__ hist) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long m =
+        nvalid_src ? (unsigned long long)nvalid_src[0] : nvalid_fixed;
+    // which 0: rank (m-1)/2 ; which 1: rank m/2  (equal for odd m)
+    st->k = which == 0 ? (m ? (m - 1) / 2 : 0) : m / 2;
+    st->prefix = 0;
+    st->mask = 0;
+    for (int j = 0; j < 256; ++j) hist[j] = 0;
+}
+
+__global__ void k_sel_finish(const SelState* __restrict__ a, const SelState* __restrict__ b,
+                             const double* __restrict__ nvalid_src,
+                             unsigned long long nvalid_fixed, double* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long m =
+        nvalid_src ? (unsigned long long)nvalid_src[0] : nvalid_fixed;
+    const double va = __longlong_as_double((long long)a->prefix);
+    const double vb = __longlong_as_double((long long)b->prefix);
+    if (m == 0) out[0] = __builtin_nan("");
+    else out[0] = (m % 2 == 0) ? (va + vb) / 2.0 : vb;
+}
+
+static unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+static int check_cam(const acm_camera* cam) {
+    if (!cam) return fail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
+    const int p = acm_num_params(cam->model);
+    if (p < 0) return fail(ACM_ERR_INVALID_MODEL, "unknown camera model id");
+    if ((int)cam->num_params != p)
+        return fail(ACM_ERR_INVALID_PARAMS, "camera num_params does not match the model");
+    return ACM_SUCCESS;
+}
+
+static int check_layout(int layout) {
+    if (layout != ACM_LAYOUT_AOS && layout != ACM_LAYOUT_SOA)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "layout must be ACM_LAYOUT_AOS or ACM_LAYOUT_SOA");
+    return ACM_SUCCESS;
+}
+
+}  // namespace acm
+
+using namespace acm;
+
+// ====================================================================== C-ABI
+extern "C" {
+
+ACM_API int acm_num_params(int model) {
+    switch (model) {
+    case ACM_PINHOLE: return 4;
+    case ACM_RADTAN: return 9;
+    case ACM_KANNALA_BRANDT: return 8;
+    case ACM_DOUBLE_SPHERE: return 6;
+    case ACM_UCM: return 5;
+    case ACM_EUCM: return 6;
+    case ACM_FOV: return 5;
+    default: return -1;
+    }
+}
+
+ACM_API int acm_validate_params(const acm_camera* cam) {
+    if (!cam) return fail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
+    const double* p = cam->params;
+    // validation::validate_intrinsics (src/camera/mod.rs:362-371)
+    if (p[0] <= 0.0 || p[1] <= 0.0) return ACM_FOCAL_LENGTH_MUST_BE_POSITIVE;
+    if (!std::isfinite(p[2]) || !std::isfinite(p[3])) return ACM_PRINCIPAL_POINT_MUST_BE_FINITE;
+    switch (cam->model) {
+    case ACM_DOUBLE_SPHERE:  // double_sphere.rs:592-607
+        if (p[4] <= 0.0 || p[4] > 1.0) return fail(ACM_INVALID_DISTORTION, "alpha must be in (0, 1]");
+        if (!std::isfinite(p[5])) return fail(ACM_INVALID_DISTORTION, "xi must be finite");
+        break;
+    case ACM_UCM:  // ucm.rs:467-477
+        if (!std::isfinite(p[4])) return fail(ACM_INVALID_DISTORTION, "alpha must be finite");
+        break;
+    case ACM_EUCM:  // eucm.rs:501-517
+        if (!std::isfinite(p[4])) return fail(ACM_INVALID_DISTORTION, "alpha must be finite");
+        if (!std::isfinite(p[5])) return fail(ACM_INVALID_DISTORTION, "beta must be finite");
+        break;
+    default: break;
+    }
+    return ACM_VALID;
+}
+
+ACM_API int acm_camera_init(acm_camera* cam, int model, const double* params, size_t num_params,
+                            uint32_t width, uint32_t height) {
+    if (!cam || (!params && num_params)) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL argument");
+    const int p = acm_num_params(model);
+    if (p < 0) return fail(ACM_ERR_INVALID_MODEL, "unknown camera model id");
+    if ((size_t)p != num_params)
+        return fail(ACM_ERR_INVALID_PARAMS, "Expected " + std::to_string(p) + " parameters, got " +
+                                                std::to_string(num_params));
+    std::memset(cam, 0, sizeof(*cam));
+    cam->model = model;
+    cam->width = width;
+    cam->height = height;
+    cam->num_params = (uint32_t)p;
+    for (int i = 0; i < p; ++i) cam->params[i] = params[i];
+    if (model == ACM_PINHOLE || model == ACM_RADTAN) {  // pinhole.rs:80, rad_tan.rs:135
+        const int v = acm_validate_params(cam);
+        if (v != ACM_VALID) return fail(ACM_ERR_INVALID_PARAMS, "validate_params failed");
+    }
+    return ACM_SUCCESS;
+}
+
+ACM_API int acm_project(const acm_camera* cam, size_t n, const double* points_3d, int layout,
+                        double* points_2d, uint8_t* status, double* jacobian, void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if ((rc = check_layout(layout))) return rc;
+    if (n == 0) return ACM_SUCCESS;
+    if (!points_3d || !points_2d || !status) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    hipStream_t s = (hipStream_t)stream;
+    return dispatch_model(cam->model, [&](auto tag) -> int {
+        using TagT = decltype(tag);
+        const dim3 g(grid_for(n)), b(kBlock);
+        if (layout == ACM_LAYOUT_AOS) {
+            if (jacobian)
+                hipLaunchKernelGGL((k_project<TagT, ACM_LAYOUT_AOS, true>), g, b, 0, s, *cam, n,
+                                   points_3d, points_2d, status, jacobian);
+            else
+                hipLaunchKernelGGL((k_project<TagT, ACM_LAYOUT_AOS, false>), g, b, 0, s, *cam, n,
+                                   points_3d, points_2d, status, jacobian);
+        } else {
+            if (jacobian)
+                hipLaunchKernelGGL((k_project<TagT, ACM_LAYOUT_SOA, true>), g, b, 0, s, *cam, n,
+                                   points_3d, points_2d, status, jacobian);
+            else
+                hipLaunchKernelGGL((k_project<TagT, ACM_LAYOUT_SOA, false>), g, b, 0, s, *cam, n,
+                                   points_3d, points_2d, status, jacobian);
+        }
+        return check_launch("acm_project");
+    });
+}
+
+ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_2d, double* rays,
+                          int layout, uint8_t* status, void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if ((rc = check_layout(layout))) return rc;
+    if (n == 0) return ACM_SUCCESS;
+    if (!points_2d || !rays || !status) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    hipStream_t s = (hipStream_t)stream;
+    return dispatch_model(cam->model, [&](auto tag) -> int {
+        using TagT = decltype(tag);
+        const dim3 g(grid_for(n)), b(kBlock);
+        if (layout == ACM_LAYOUT_AOS)
+            hipLaunchKernelGGL((k_unproject<TagT, ACM_LAYOUT_AOS>), g, b, 0, s, *cam, n, points_2d,
+                               rays, status);
+        else
+            hipLaunchKernelGGL((k_unproject<TagT, ACM_LAYOUT_SOA>), g, b, 0, s, *cam, n, points_2d,
+                               rays, status);
+        return check_launch("acm_unproject");
+    });
+}
+
+ACM_API int acm_residual_jacobian(const acm_camera* cam, size_t n, const double* points_3d,
+                                  int layout, const double* points_2d_obs, int invalid_policy,
+                                  double* residual, double* jacobian, uint8_t* status,
+                                  void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if ((rc = check_layout(layout))) return rc;
+    if (invalid_policy != ACM_INVALID_SKIP && invalid_policy != ACM_INVALID_SENTINEL)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "invalid_policy must be SKIP or SENTINEL");
+    if (n == 0) return ACM_SUCCESS;
+    if (!points_3d || !points_2d_obs || !residual)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    hipStream_t s = (hipStream_t)stream;
+    return dispatch_model(cam->model, [&](auto tag) -> int {
+        using TagT = decltype(tag);
+        const dim3 g(grid_for(n)), b(kBlock);
+#define ACM_LAUNCH_RES(L, WJ)                                                                   \
+    hipLaunchKernelGGL((k_residual<TagT, L, WJ>), g, b, 0, s, *cam, n, points_3d, points_2d_obs, \
+                       invalid_policy, residual, jacobian, status)
+        if (layout == ACM_LAYOUT_AOS) {
+            if (jacobian) ACM_LAUNCH_RES(ACM_LAYOUT_AOS, true);
+            else ACM_LAUNCH_RES(ACM_LAYOUT_AOS, false);
+        } else {
+            if (jacobian) ACM_LAUNCH_RES(ACM_LAYOUT_SOA, true);
+            else ACM_LAUNCH_RES(ACM_LAYOUT_SOA, false);
+        }
+#undef ACM_LAUNCH_RES
+        return check_launch("acm_residual_jacobian");
+    });
+}
+
+ACM_API size_t acm_normal_equations_workspace_size(int model, size_t n) {
+    const int P = acm_num_params(model);
+    if (P < 0) return 0;
+    const int K = P * (P + 1) / 2 + P + 2;
+    return ((size_t)ne_blocks(n) + 1) * (size_t)K * sizeof(double);
+}
+
+ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* points_3d,
+                                 int layout, const double* points_2d_obs, int invalid_policy,
+                                 double* result, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if ((rc = check_layout(layout))) return rc;
+    if (invalid_policy != ACM_INVALID_SKIP && invalid_policy != ACM_INVALID_SENTINEL)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "invalid_policy must be SKIP or SENTINEL");
+    if (!result || !workspace || (n && (!points_3d || !points_2d_obs)))
+        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_normal_equations_workspace_size(cam->model, n))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "normal-equations workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = ne_blocks(n);
+    return dispatch_model(cam->model, [&](auto tag) -> int {
+        using TagT = decltype(tag);
+        using M = typename TagT::template type<double>;
+        constexpr int P = M::P;
+        constexpr int K = NE<P>::K;
+        double* parts = (double*)workspace;
+        double* sums = parts + (size_t)nb * K;
+        if (layout == ACM_LAYOUT_AOS)
+            hipLaunchKernelGGL((k_normal_eq<TagT, ACM_LAYOUT_AOS>), dim3(nb), dim3(kBlock), 0, s,
+                               *cam, n, points_3d, points_2d_obs, invalid_policy, parts);
+        else
+            hipLaunchKernelGGL((k_normal_eq<TagT, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s,
+                               *cam, n, points_3d, points_2d_obs, invalid_policy, parts);
+        hipLaunchKernelGGL(k_sum_columns, dim3(K), dim3(kBlock), 0, s, parts, nb, K, sums);
+        hipLaunchKernelGGL(k_ne_expand, dim3(1), dim3(64), 0, s, sums, P, result);
+        return check_launch("acm_normal_equations");
+    });
+}
+
+ACM_API size_t acm_reprojection_stats_workspace_size(size_t n) {
+    // errors (N) + pass-1 partials (nb*5) + totals (5) + pass-2 partials (nb) + var (1)
+    const size_t nb = (size_t)ne_blocks(n);
+    return (n + nb * 5 + 5 + nb + 1) * sizeof(double);
+}
+
+ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double* points_3d,
+                                   int layout, const double* points_2d, double* result,
+                                   double* errors, void* workspace, size_t workspace_bytes,
+                                   void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if ((rc = check_layout(layout))) return rc;
+    if (!result || !workspace || (n && (!points_3d || !points_2d)))
+        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_reprojection_stats_workspace_size(n))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "reprojection-stats workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = ne_blocks(n);
+    double* ws = (double*)workspace;
+    double* errs = errors ? errors : ws;
+    double* p1 = ws + n;
+    double* tot = p1 + (size_t)nb * 5;
+    double* p2 = tot + 5;
+    double* var = p2 + nb;
+    return dispatch_model(cam->model, [&](auto tag) -> int {
+        using TagT = decltype(tag);
+        if (layout == ACM_LAYOUT_AOS)
+            hipLaunchKernelGGL((k_reproj_pass1<TagT, ACM_LAYOUT_AOS>), dim3(nb), dim3(kBlock), 0, s,
+                               *cam, n, points_3d, points_2d, errs, p1);
+        else
+            hipLaunchKernelGGL((k_reproj_pass1<TagT, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s,
+                               *cam, n, points_3d, points_2d, errs, p1);
+        hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb, tot);
+        hipLaunchKernelGGL(k_reproj_pass2, dim3(nb), dim3(kBlock), 0, s, n, errs, tot, p2);
+        hipLaunchKernelGGL(k_sum_columns, dim3(1), dim3(kBlock), 0, s, p2, nb, 1, var);
+        hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, var, result);
+        return check_launch("acm_reprojection_stats");
+    });
+}
+
+ACM_API int acm_sample_points_grid(uint32_t width, uint32_t height, size_t n_requested,
+                                   uint32_t* num_cells_x, uint32_t* num_cells_y) {
+    if (!num_cells_x || !num_cells_y) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL argument");
+    const double w = (double)width, h = (double)height;  // point_sampling.rs:50-54
+    const double fx = std::round(std::sqrt((double)n_requested * (w / h)));
+    const double fy = std::round(std::sqrt((double)n_requested * (h / w)));
+    if (!(fx >= 1.0) || !(fy >= 1.0) || fx > 4e9 || fy > 4e9)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "sample grid is empty or too large");
+    *num_cells_x = (uint32_t)fx;
+    *num_cells_y = (uint32_t)fy;
+    return ACM_SUCCESS;
+}
+
+ACM_API size_t acm_sample_points_workspace_size(const acm_camera* cam, size_t n_requested) {
+    uint32_t ncx, ncy;
+    if (!cam || acm_sample_points_grid(cam->width, cam->height, n_requested, &ncx, &ncy))
+        return 0;
+    const size_t nb = ((size_t)ncx * ncy + kBlock - 1) / kBlock;
+    return 2 * nb * sizeof(uint64_t);
+}
+
+ACM_API int acm_sample_points(const acm_camera* cam, size_t n_requested, double* points_2d_out,
+                              double* points_3d_out, uint64_t* counts, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    uint32_t ncx, ncy;
+    if ((rc = acm_sample_points_grid(cam->width, cam->height, n_requested, &ncx, &ncy))) return rc;
+    if (!points_2d_out || !points_3d_out || !counts || !workspace)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_sample_points_workspace_size(cam, n_requested))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "sample_points workspace too small");
+    const size_t cells = (size_t)ncx * ncy;
+    const size_t nb = (cells + kBlock - 1) / kBlock;
+    if (nb > 0x7fffffffull) return fail(ACM_ERR_INVALID_ARGUMENT, "sample grid too large");
+    Grid g;
+    g.ncx = ncx;
+    g.ncy = ncy;
+    g.cw = (double)cam->width / (double)ncx;  // :57
+    g.ch = (double)cam->height / (double)ncy;
+    uint64_t* cnt = (uint64_t*)workspace;
+    uint64_t* off = cnt + nb;
+    hipStream_t s = (hipStream_t)stream;
+    return dispatch_model(cam->model, [&](auto tag) -> int {
+        using TagT = decltype(tag);
+        hipLaunchKernelGGL((k_sample_count<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, *cam,
+                           g, cells, cnt);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, cnt, nb, off, counts,
+                           (uint64_t)cells);
+        hipLaunchKernelGGL((k_sample_write<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, *cam,
+                           g, cells, off, points_2d_out, points_3d_out);
+        return check_launch("acm_sample_points");
+    });
+}
+
+ACM_API size_t acm_median_workspace_size(size_t n) {
+    (void)n;
+    return 2 * sizeof(SelState) + 256 * sizeof(unsigned long long);
+}
+
+ACM_API int acm_median_valid(size_t n, const double* values, const double* n_valid_device,
+                             uint64_t n_valid, double* out, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+    if (!out || !workspace || (n && !values)) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_median_workspace_size(n))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "median workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    SelState* sa = (SelState*)workspace;
+    SelState* sb = sa + 1;
+    unsigned long long* hist = (unsigned long long*)(sb + 1);
+    const unsigned nb = (unsigned)ne_blocks(n);
+    for (int which = 0; which < 2; ++which) {
+        SelState* st = which ? sb : sa;
+        hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, s, st, n_valid_device,
+                           (unsigned long long)n_valid, which, hist);
+        for (int shift = 56; shift >= 0; shift -= 8) {
+            hipLaunchKernelGGL(k_sel_hist, dim3(nb), dim3(kBlock), 0, s, n, values, st, shift,
+                               hist);
+            hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(64), 0, s, st, shift, hist);
+        }
+    }
+    hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(64), 0, s, sa, sb, n_valid_device,
+                       (unsigned long long)n_valid, out);
+    return check_launch("acm_median_valid");
+}
+
+ACM_API int acm_last_hip_error(void) { return g_last_hip_error; }
+ACM_API const char* acm_last_error(void) { return g_last_error.c_str(); }
+ACM_API const char* acm_version(void) { return "acm 0.1.0 (gfx950)"; }
+
+}  // extern "C"

@@ -1,0 +1,473 @@
+// camera_models.hpp -- per-point device math of the seven camera models.
+//
+// Each model is a struct of __device__ functions templated on the scalar T
+// (double for the parity path, float for the f32 tolerance sweep).  The
+// arithmetic follows the reference Rust code expression by expression (Rust
+// evaluates `a + b + c` as (a + b) + c and never contracts to FMA; this file
+// is compiled with -ffp-contract=off so hipcc does not either), which is what
+// makes the validity masks bit-exact: every threshold test sees the same
+// doubles as the reference.  Divisions and square roots are the IEEE
+// correctly-rounded f64 sequences hipcc emits by default (no -ffast-math).
+// Only atan2/sin/cos/tan (OCML) can differ from glibc by ulps, and no status
+// decision depends on them.
+//
+// Status decisions are computed branch-free where possible so a wave does
+// not diverge on the rare failing point; the caller selects outputs.
+//
+// Reference citations: /root/reference/src/camera/<model>.rs:line.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace acm {
+
+enum : uint8_t {
+    ST_OK = 0,
+    ST_PROJECTION_OUT_SIDE_IMAGE = 1,
+    ST_POINT_IS_OUT_SIDE_IMAGE = 2,
+    ST_POINT_AT_CAMERA_CENTER = 3,
+    ST_NUMERICAL_ERROR = 4,
+};
+
+constexpr double kEps = 2.220446049250313e-16;      // f64::EPSILON
+constexpr double kEpsSqrt = 1.4901161193847656e-08;  // f64::EPSILON.sqrt()
+constexpr double kPi = 3.141592653589793;
+
+// Uniform camera parameters, converted once per thread from the kernel
+// argument (they stay in SGPRs: every lane reads the same values).
+template <class T>
+struct Cam {
+    T p[9];
+    T w, h;        // resolution as f64, like `width as f64` in the reference
+    uint32_t wi, hi;
+};
+
+// ---------------------------------------------------------------- Pinhole
+template <class T>
+struct Pinhole {
+    static constexpr int P = 4;
+    // pinhole.rs:165-182
+    template <bool WJ>
+    __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
+                                                      T& v, T* ju, T* jv) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        u = fx * x / z + cx;  // :170
+        v = fy * y / z + cy;  // :171
+        uint8_t st = ST_OK;
+        if (u < T(0) || u >= c.w || v < T(0) || v >= c.h) st = ST_PROJECTION_OUT_SIDE_IMAGE;
+        if (z < T(kEpsSqrt)) st = ST_POINT_AT_CAMERA_CENTER;  // :167, checked first
+        if (WJ) {
+            ju[0] = x / z; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
+            jv[0] = T(0); jv[1] = y / z; jv[2] = T(0); jv[3] = T(1);
+        }
+        return st;
+    }
+    // pinhole.rs:228-246
+    __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
+                                                        T& Z) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const bool out = u < T(0) || u >= c.w || v < T(0) || v >= c.h;
+        T mx = (u - cx) / fx;
+        T my = (v - cy) / fy;
+        T r2 = mx * mx + my * my;
+        T norm = sqrt(T(1) + r2);
+        T ninv = T(1) / norm;
+        X = mx * ninv;
+        Y = my * ninv;
+        Z = ninv;
+        return out ? ST_POINT_IS_OUT_SIDE_IMAGE : ST_OK;
+    }
+};
+
+// ----------------------------------------------------------------- RadTan
+template <class T>
+struct RadTan {
+    static constexpr int P = 9;  // fx fy cx cy k1 k2 p1 p2 k3
+    // rad_tan.rs:302-348
+    template <bool WJ>
+    __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
+                                                      T& v, T* ju, T* jv) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const T k1 = c.p[4], k2 = c.p[5], p1 = c.p[6], p2 = c.p[7], k3 = c.p[8];
+        T xp = x / z, yp = y / z;
+        T r2 = xp * xp + yp * yp;
+        T r4 = r2 * r2;
+        T r6 = r4 * r2;
+        T radial = T(1) + k1 * r2 + k2 * r4 + k3 * r6;
+        T xd = xp * radial + T(2) * p1 * xp * yp + p2 * (r2 + T(2) * xp * xp);
+        T yd = yp * radial + p1 * (r2 + T(2) * yp * yp) + T(2) * p2 * xp * yp;
+        u = fx * xd + cx;
+        v = fy * yd + cy;
+        uint8_t st = ST_OK;
+        if (u < T(0) || u >= c.w || v < T(0) || v >= c.h) st = ST_PROJECTION_OUT_SIDE_IMAGE;
+        if (z < T(kEpsSqrt)) st = ST_POINT_AT_CAMERA_CENTER;  // :304
+        if (WJ) {
+            T xpyp2 = T(2) * xp * yp;
+            ju[0] = xd; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
+            ju[4] = fx * xp * r2;
+            ju[5] = fx * xp * r4;
+            ju[6] = fx * xpyp2;
+            ju[7] = fx * (r2 + T(2) * xp * xp);
+            ju[8] = fx * xp * r6;
+            jv[0] = T(0); jv[1] = yd; jv[2] = T(0); jv[3] = T(1);
+            jv[4] = fy * yp * r2;
+            jv[5] = fy * yp * r4;
+            jv[6] = fy * (r2 + T(2) * yp * yp);
+            jv[7] = fy * xpyp2;
+            jv[8] = fy * yp * r6;
+        }
+        return st;
+    }
+    // rad_tan.rs:401-524: Newton on the 2x2 distortion Jacobian, <=100 steps.
+    __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
+                                                        T& Z) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const T k1 = c.p[4], k2 = c.p[5], p1 = c.p[6], p2 = c.p[7], k3 = c.p[8];
+        if (u < T(0) || u >= c.w || v < T(0) || v >= c.h) {
+            X = Y = Z = T(NAN);
+            return ST_POINT_IS_OUT_SIDE_IMAGE;
+        }
+        const T tx = (u - cx) / fx;
+        const T ty = (v - cy) / fy;
+        T px = tx, py = ty;
+        const T EPS = T(1e-6);
+        uint8_t st = ST_OK;
+        for (unsigned it = 0; it < 100u; ++it) {
+            T x = px, y = py;
+            T r2 = x * x + y * y;
+            T r4 = r2 * r2;
+            T r6 = r4 * r2;
+            T rad = T(1) + k1 * r2 + k2 * r4 + k3 * r6;
+            T xe = x * rad + T(2) * p1 * x * y + p2 * (r2 + T(2) * x * x);
+            T ye = y * rad + p1 * (r2 + T(2) * y * y) + T(2) * p2 * x * y;
+            T ex = xe - tx, ey = ye - ty;
+            if (sqrt(ex * ex + ey * ey) < EPS) break;  // :459
+            T drdx = T(2) * x, drdy = T(2) * y;
+            T ddx = (k1 + T(2) * k2 * r2 + T(3) * k3 * r4) * drdx;
+            T ddy = (k1 + T(2) * k2 * r2 + T(3) * k3 * r4) * drdy;
+            T j00 = rad + x * ddx + T(2) * p1 * y + p2 * (drdx + T(4) * x);
+            T j01 = x * ddy + T(2) * p1 * x + p2 * (drdy);
+            T j10 = y * ddx + p1 * (drdx) + T(2) * p2 * y;
+            T j11 = rad + y * ddy + p1 * (drdy + T(4) * y) + T(2) * p2 * x;
+            // nalgebra Matrix2::try_inverse: det = m11*m22 - m21*m12
+            T det = j00 * j11 - j10 * j01;
+            if (det == T(0)) { st = ST_NUMERICAL_ERROR; break; }
+            T i00 = j11 / det, i01 = -j01 / det;
+            T i10 = -j10 / det, i11 = j00 / det;
+            T dx = i00 * ex + i01 * ey;
+            T dy = i10 * ex + i11 * ey;
+            px = px - dx;
+            py = py - dy;
+            if (sqrt(dx * dx + dy * dy) < EPS) break;  // :503
+            if (it == 99u) st = ST_NUMERICAL_ERROR;    // :514
+        }
+        T n = sqrt(px * px + py * py + T(1) * T(1));
+        X = px / n;
+        Y = py / n;
+        Z = T(1) / n;
+        return st;
+    }
+};
+
+// --------------------------------------------------------- Kannala-Brandt
+template <class T>
+struct KannalaBrandt {
+    static constexpr int P = 8;  // fx fy cx cy k1 k2 k3 k4
+    // kannala_brandt.rs:340-394
+    template <bool WJ>
+    __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
+                                                      T& v, T* ju, T* jv) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const T k1 = c.p[4], k2 = c.p[5], k3 = c.p[6], k4 = c.p[7];
+        uint8_t st = z < T(0) ? ST_POINT_IS_OUT_SIDE_IMAGE
+                              : (z < T(kEps) ? ST_POINT_AT_CAMERA_CENTER : ST_OK);
+        T r = sqrt(x * x + y * y);  // :363-364
+        T theta = atan2(r, z);      // :365
+        T theta2 = theta * theta;
+        T theta3 = theta2 * theta;
+        T theta5 = theta3 * theta2;
+        T theta7 = theta5 * theta2;
+        T theta9 = theta7 * theta2;
+        T theta_d = theta + k1 * theta3 + k2 * theta5 + k3 * theta7 + k4 * theta9;
+        const bool axis = r < T(kEps);  // :375
+        T x_r = axis ? T(0) : x / r;
+        T y_r = axis ? T(0) : y / r;
+        u = fx * theta_d * x_r + cx;  // :390
+        v = fy * theta_d * y_r + cy;
+        if (WJ) {
+            T fxr = fx * x_r, fyr = fy * y_r;
+            ju[0] = theta_d * x_r; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
+            ju[4] = fxr * theta3; ju[5] = fxr * theta5; ju[6] = fxr * theta7; ju[7] = fxr * theta9;
+            jv[0] = T(0); jv[1] = theta_d * y_r; jv[2] = T(0); jv[3] = T(1);
+            jv[4] = fyr * theta3; jv[5] = fyr * theta5; jv[6] = fyr * theta7; jv[7] = fyr * theta9;
+        }
+        return st;
+    }
+    // kannala_brandt.rs:445-562: Newton on theta_d(theta) = ru, <=10 steps.
+    __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
+                                                        T& Z) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const T k1 = c.p[4], k2 = c.p[5], k3 = c.p[6], k4 = c.p[7];
+        if (c.wi > 0 && c.hi > 0 && (u < T(0) || u >= c.w || v < T(0) || v >= c.h)) {
+            X = Y = Z = T(NAN);
+            return ST_POINT_IS_OUT_SIDE_IMAGE;  // :447-455
+        }
+        T mx = (u - cx) / fx;
+        T my = (v - cy) / fy;
+        T ru = sqrt(mx * mx + my * my);
+        ru = fmin(ru, T(kPi / 2.0));  // :467, f64::min semantics
+        T theta = ru;
+        const T PREC = T(1e-6);
+        bool converged = true;
+        if (ru > PREC) {
+            for (int i = 0; i < 10; ++i) {
+                T theta2 = theta * theta;
+                T theta4 = theta2 * theta2;
+                T theta6 = theta4 * theta2;
+                T theta8 = theta4 * theta4;
+                T k1t2 = k1 * theta2, k2t4 = k2 * theta4, k3t6 = k3 * theta6, k4t8 = k4 * theta8;
+                T f = theta * (T(1) + k1t2 + k2t4 + k3t6 + k4t8) - ru;
+                T fp = T(1) + (T(3) * k1t2) + (T(5) * k2t4) + (T(7) * k3t6) + (T(9) * k4t8);
+                if (fabs(fp) < T(kEps)) { converged = false; break; }
+                T delta = f / fp;
+                theta -= delta;
+                if (fabs(delta) < PREC) break;
+                if (i == 9) converged = false;
+            }
+        } else {
+            if (ru > T(0)) converged = false;
+            else { theta = T(0); }
+        }
+        const bool small = fabs(ru) < T(kEps);
+        T xc = small ? T(0) : mx / ru;
+        T yc = small ? T(0) : my / ru;
+        T s = sin(theta), co = cos(theta);
+        T px = s * xc, py = s * yc;
+        T n = sqrt(px * px + py * py + co * co);
+        X = px / n;
+        Y = py / n;
+        Z = co / n;
+        return converged ? ST_OK : ST_NUMERICAL_ERROR;
+    }
+};
+
+// ---------------------------------------------------------- Double Sphere
+template <class T>
+struct DoubleSphere {
+    static constexpr int P = 6;  // fx fy cx cy alpha xi
+    // double_sphere.rs:361-390 + check_projection_condition :177-184
+    template <bool WJ>
+    __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
+                                                      T& v, T* ju, T* jv) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const T alpha = c.p[4], xi = c.p[5];
+        T r_squared = (x * x) + (y * y);
+        T d1 = sqrt(r_squared + (z * z));
+        T gamma = xi * d1 + z;
+        T d2 = sqrt(r_squared + gamma * gamma);
+        T denom = alpha * d2 + (T(1) - alpha) * gamma;
+        // w1, w2 are camera constants (uniform -> scalar unit)
+        T w1 = alpha <= T(0.5) ? alpha / (T(1) - alpha) : (T(1) - alpha) / alpha;
+        T w2 = (w1 + xi) / sqrt(T(2) * w1 * xi + xi * xi + T(1));
+        const bool ok = !(denom < T(1e-3)) && (z > -w2 * d1);
+        T mx = x / denom, my = y / denom;
+        u = fx * (mx) + cx;
+        v = fy * (my) + cy;
+        if (WJ) {
+            T tu = fx * mx / denom, tv = fy * my / denom;
+            T dda = d2 - gamma;
+            T ddx = d1 * (alpha * gamma / d2 + (T(1) - alpha));
+            ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
+            ju[4] = -tu * dda; ju[5] = -tu * ddx;
+            jv[0] = T(0); jv[1] = my; jv[2] = T(0); jv[3] = T(1);
+            jv[4] = -tv * dda; jv[5] = -tv * ddx;
+        }
+        return ok ? ST_OK : ST_POINT_IS_OUT_SIDE_IMAGE;
+    }
+    // double_sphere.rs:436-476 + check_unprojection_condition :200-209
+    __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
+                                                        T& Z) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const T alpha = c.p[4], xi = c.p[5];
+        T gamma_ds = T(1) - alpha;
+        T mx = (u - cx) / fx;
+        T my = (v - cy) / fy;
+        T r_squared = (mx * mx) + (my * my);
+        const bool cond = !(alpha > T(0.5) && r_squared > T(1) / (T(2) * alpha - T(1)));
+        const bool reject = alpha != T(0) && !cond;
+        T mz = (T(1) - alpha * alpha * r_squared) /
+               (alpha * sqrt(T(1) - (T(2) * alpha - T(1)) * r_squared) + gamma_ds);
+        T mz_squared = mz * mz;
+        T num = mz * xi + sqrt(mz_squared + (T(1) - xi * xi) * r_squared);
+        T denom = mz_squared + r_squared;
+        T coeff = num / denom;
+        T px = coeff * mx, py = coeff * my, pz = coeff * mz - xi;
+        T n = sqrt(px * px + py * py + pz * pz);
+        X = px / n;
+        Y = py / n;
+        Z = pz / n;
+        return (reject || denom < T(1e-3)) ? ST_POINT_IS_OUT_SIDE_IMAGE : ST_OK;
+    }
+};
+
+// -------------------------------------------------------------------- UCM
+template <class T>
+struct Ucm {
+    static constexpr int P = 5;  // fx fy cx cy alpha
+    // ucm.rs:297-316 + check_proj_condition :154-161
+    template <bool WJ>
+    __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
+                                                      T& v, T* ju, T* jv) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], alpha = c.p[4];
+        T d = sqrt(x * x + y * y + z * z);
+        T denom = alpha * d + (T(1) - alpha) * z;
+        T w = alpha <= T(0.5) ? alpha / (T(1) - alpha) : (T(1) - alpha) / alpha;
+        const bool ok = !(denom < T(1e-3)) && (z > -w * d);
+        T mx = x / denom, my = y / denom;
+        u = fx * mx + cx;
+        v = fy * my + cy;
+        if (WJ) {
+            T tu = fx * mx / denom, tv = fy * my / denom;
+            T dda = d - z;
+            ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0); ju[4] = -tu * dda;
+            jv[0] = T(0); jv[1] = my; jv[2] = T(0); jv[3] = T(1); jv[4] = -tv * dda;
+        }
+        return ok ? ST_OK : ST_POINT_IS_OUT_SIDE_IMAGE;
+    }
+    // ucm.rs:337-367 (+ :177-184); keeps the reference's denom = 1 - r^2 (:354)
+    __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
+                                                        T& Z) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], alpha = c.p[4];
+        T gamma = T(1) - alpha;
+        T xi = alpha / gamma;
+        T mx = (u - cx) / fx * gamma;
+        T my = (v - cy) / fy * gamma;
+        T r_squared = mx * mx + my * my;
+        T num = xi + sqrt(T(1) + (T(1) - xi * xi) * r_squared);
+        T denom = T(1) - r_squared;
+        const bool cond = alpha > T(0.5) ? (r_squared <= gamma * gamma / (T(2) * alpha - T(1)))
+                                         : true;
+        T coeff = num / denom;
+        T px = coeff * mx, py = coeff * my, pz = coeff - xi;
+        T n = sqrt(px * px + py * py + pz * pz);
+        X = px / n;
+        Y = py / n;
+        Z = pz / n;
+        return (denom < T(1e-3) || !cond) ? ST_POINT_IS_OUT_SIDE_IMAGE : ST_OK;
+    }
+};
+
+// ------------------------------------------------------------------- EUCM
+template <class T>
+struct Eucm {
+    static constexpr int P = 6;  // fx fy cx cy alpha beta
+    // eucm.rs:328-347 + check_proj_condition :167-177
+    template <bool WJ>
+    __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
+                                                      T& v, T* ju, T* jv) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const T alpha = c.p[4], beta = c.p[5];
+        T rr = x * x + y * y;
+        T d = sqrt(beta * rr + z * z);
+        T denom = alpha * d + (T(1) - alpha) * z;
+        bool cond = true;
+        if (alpha > T(0.5)) {
+            T cc = (alpha - T(1)) / (T(2) * alpha - T(1));
+            cond = !(z < denom * cc);
+        }
+        const bool ok = !(denom < T(1e-3)) && cond;
+        T mx = x / denom, my = y / denom;
+        u = fx * mx + cx;
+        v = fy * my + cy;
+        if (WJ) {
+            T tu = fx * mx / denom, tv = fy * my / denom;
+            T dda = d - z;
+            T ddb = alpha * rr / (T(2) * d);
+            ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
+            ju[4] = -tu * dda; ju[5] = -tu * ddb;
+            jv[0] = T(0); jv[1] = my; jv[2] = T(0); jv[3] = T(1);
+            jv[4] = -tv * dda; jv[5] = -tv * ddb;
+        }
+        return ok ? ST_OK : ST_POINT_IS_OUT_SIDE_IMAGE;
+    }
+    // eucm.rs:368-398 (+ :194-200 precedence quirk (1/beta)*(2a-1))
+    __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
+                                                        T& Z) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const T alpha = c.p[4], beta = c.p[5];
+        T mx = (u - cx) / fx;
+        T my = (v - cy) / fy;
+        T r_squared = mx * mx + my * my;
+        T gamma = T(1) - alpha;
+        T num = T(1) - r_squared * alpha * alpha * beta;
+        T det = T(1) - (alpha - gamma) * beta * r_squared;
+        T denom = gamma + alpha * sqrt(det);
+        const bool cond = !(alpha > T(0.5) && r_squared > (T(1) / beta * (T(2) * alpha - T(1))));
+        T mz = num / denom;
+        T n = sqrt(mx * mx + my * my + mz * mz);
+        X = mx / n;
+        Y = my / n;
+        Z = mz / n;
+        return (det < T(1e-3) || !cond) ? ST_POINT_IS_OUT_SIDE_IMAGE : ST_OK;
+    }
+};
+
+// -------------------------------------------------------------------- FOV
+template <class T>
+struct Fov {
+    static constexpr int P = 5;  // fx fy cx cy w
+    // fov.rs:284-316
+    template <bool WJ>
+    __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
+                                                      T& v, T* ju, T* jv) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], wf = c.p[4];
+        T r2 = x * x + y * y;
+        T r = sqrt(r2);
+        T tan_w_half = tan(wf / T(2));  // camera constant
+        T atan_wrd = atan2(T(2) * tan_w_half * r, z);
+        const bool axis = r2 < T(kEpsSqrt);
+        T rd = axis ? T(2) * tan_w_half / wf : atan_wrd / (r * wf);
+        T mx = x * rd, my = y * rd;
+        u = fx * mx + cx;
+        v = fy * my + cy;
+        if (WJ) {
+            T drd;
+            if (axis) {
+                drd = ((T(1) + tan_w_half * tan_w_half) * wf - T(2) * tan_w_half) / (wf * wf);
+            } else {
+                T a = T(2) * tan_w_half * r;
+                T datan = z * r * (T(1) + tan_w_half * tan_w_half) / (a * a + z * z);
+                drd = datan / (r * wf) - atan_wrd / (r * wf * wf);
+            }
+            ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0); ju[4] = fx * x * drd;
+            jv[0] = T(0); jv[1] = my; jv[2] = T(0); jv[3] = T(1); jv[4] = fy * y * drd;
+        }
+        return z < T(kEpsSqrt) ? ST_POINT_AT_CAMERA_CENTER : ST_OK;
+    }
+    // fov.rs:336-363
+    __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
+                                                        T& Z) {
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], wf = c.p[4];
+        T tan_w_2 = tan(wf / T(2));
+        T mul2 = tan_w_2 * T(2);
+        T mx = (u - cx) / fx;
+        T my = (v - cy) / fy;
+        T rd = sqrt(mx * mx + my * my);
+        T px = mx, py = my;
+        if (mul2 > T(kEpsSqrt) && rd > T(kEpsSqrt)) {
+            T srw = sin(rd * wf), crw = cos(rd * wf);
+            T ru = srw / (rd * mul2);
+            px = mx * ru / crw;
+            py = my * ru / crw;
+        }
+        T n = sqrt(px * px + py * py + T(1) * T(1));
+        X = px / n;
+        Y = py / n;
+        Z = T(1) / n;
+        return ST_OK;
+    }
+};
+
+}  // namespace acm

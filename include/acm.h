@@ -1,0 +1,214 @@
+/*
+ * acm.h -- C-ABI of the MI355X-native batched camera-model engine (libacm.so).
+ *
+ * Drop-in boundary for the reference's one data-parallel hot path
+ * (amin-abouee/apex-camera-models v0.4.1, a pure-Rust crate):
+ *
+ *   trait CameraModel::project    src/camera/mod.rs:256   (per point, Result)
+ *   trait CameraModel::unproject  src/camera/mod.rs:271   (per point, Result)
+ *   apex_solver::factors::*CameraParamsFactor  (residual 2N + Jacobian 2N x P,
+ *       constructed at bin/camera_converter.rs:378,513,652,794,925,1058)
+ *   util::compute_reprojection_error   src/util/error_metrics.rs:62-121
+ *   util::sample_points                src/util/point_sampling.rs:46-120
+ *
+ * Every entry point is batched (a per-point FFI call would be latency bound),
+ * takes plain pointers and sizes, never allocates on the hot path, and is
+ * stream-ordered on the caller's HIP stream (`void *stream`, NULL = default
+ * stream).  All point/ray/residual/Jacobian buffers are DEVICE pointers owned
+ * by the caller (hipMalloc'd or from any allocator on the same HIP runtime).
+ *
+ * Memory layouts (all f64):
+ *   points_3d  ACM_LAYOUT_AOS: nalgebra Matrix3xX column-major [x0 y0 z0 x1 ..]
+ *              ACM_LAYOUT_SOA: three planes [x0..x(N-1) | y0.. | z0..]
+ *   points_2d  nalgebra Matrix2xX column-major [u0 v0 u1 v1 ..]
+ *   jacobian   nalgebra DMatrix 2N x P column-major: entry (2i+r, p) at
+ *              jacobian[p*2N + 2i + r], r=0 for u, r=1 for v.  Parameter order
+ *              is the factor's (camera_converter.rs:385-392, :520-529, ...).
+ *   status     one uint8 per point, values acm_point_status below.
+ *
+ * Return codes: ACM_SUCCESS (0) or a negative acm_result.
+ */
+#ifndef ACM_H
+#define ACM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__GNUC__)
+#define ACM_API __attribute__((visibility("default")))
+#else
+#define ACM_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Camera model ids.  Parameter vectors (factor order):
+ *   PINHOLE  fx fy cx cy                       (src/camera/pinhole.rs)
+ *   RADTAN   fx fy cx cy k1 k2 p1 p2 k3        (src/camera/rad_tan.rs)
+ *   KB       fx fy cx cy k1 k2 k3 k4           (src/camera/kannala_brandt.rs)
+ *   DS       fx fy cx cy alpha xi              (src/camera/double_sphere.rs)
+ *   UCM      fx fy cx cy alpha                 (src/camera/ucm.rs)
+ *   EUCM     fx fy cx cy alpha beta            (src/camera/eucm.rs)
+ *   FOV      fx fy cx cy w                     (src/camera/fov.rs)          */
+typedef enum acm_model {
+    ACM_PINHOLE = 0,
+    ACM_RADTAN = 1,
+    ACM_KANNALA_BRANDT = 2,
+    ACM_DOUBLE_SPHERE = 3,
+    ACM_UCM = 4,
+    ACM_EUCM = 5,
+    ACM_FOV = 6
+} acm_model;
+
+/* Per-point status, mirroring the CameraModelError variants a projection or
+ * unprojection can return (src/camera/mod.rs:80-113). */
+typedef enum acm_point_status {
+    ACM_STATUS_OK = 0,
+    ACM_STATUS_PROJECTION_OUT_SIDE_IMAGE = 1, /* ProjectionOutSideImage */
+    ACM_STATUS_POINT_IS_OUT_SIDE_IMAGE = 2,   /* PointIsOutSideImage */
+    ACM_STATUS_POINT_AT_CAMERA_CENTER = 3,    /* PointAtCameraCenter */
+    ACM_STATUS_NUMERICAL_ERROR = 4            /* NumericalError(_) */
+} acm_point_status;
+
+/* Function results.  The positive CameraModelError codes returned by
+ * acm_validate_params mirror mod.rs:80-113 variant order + 1. */
+typedef enum acm_result {
+    ACM_SUCCESS = 0,
+    ACM_ERR_INVALID_MODEL = -1,
+    ACM_ERR_INVALID_PARAMS = -2, /* CameraModelError::InvalidParams */
+    ACM_ERR_INVALID_ARGUMENT = -3,
+    ACM_ERR_HIP = -4,
+    ACM_ERR_WORKSPACE_TOO_SMALL = -5,
+    ACM_ERR_NOT_SUPPORTED = -6
+} acm_result;
+
+typedef enum acm_validation {
+    ACM_VALID = 0,
+    ACM_FOCAL_LENGTH_MUST_BE_POSITIVE = 4, /* FocalLengthMustBePositive */
+    ACM_PRINCIPAL_POINT_MUST_BE_FINITE = 5, /* PrincipalPointMustBeFinite */
+    ACM_INVALID_DISTORTION = 6             /* InvalidParams(alpha/xi/beta) */
+} acm_validation;
+
+enum { ACM_LAYOUT_AOS = 0, ACM_LAYOUT_SOA = 1 };
+
+/* Invalid-point policy of the factor evaluation (apex-solver source absent:
+ * "skip" matches compute_reprojection_error skipping failed projections,
+ * error_metrics.rs:76; "sentinel" is the (1e6,1e6) residual of the removed
+ * in-tree factor, doc/COMPREHENSIVE_ANALYSIS.md:116-121).  J = 0 in both. */
+enum { ACM_INVALID_SKIP = 0, ACM_INVALID_SENTINEL = 1 };
+
+#define ACM_MAX_PARAMS 9
+
+/* A camera: model id, resolution and the factor-order parameter vector.
+ * Replaces the model structs (e.g. KannalaBrandtModel,
+ * kannala_brandt.rs:65-72).  Passed by value into every kernel, so the
+ * parameters live in SGPRs (uniform across the wave), not in HBM or LDS. */
+typedef struct acm_camera {
+    int32_t model;
+    uint32_t width;
+    uint32_t height;
+    uint32_t num_params;
+    double params[ACM_MAX_PARAMS];
+} acm_camera;
+
+/* Number of parameters of a model (Pinhole 4 .. RadTan 9), or -1. */
+ACM_API int acm_num_params(int model);
+
+/* Fill *cam.  Mirrors XModel::new(&DVector): wrong parameter count ->
+ * ACM_ERR_INVALID_PARAMS (kannala_brandt.rs:122-128, pinhole.rs:60-66, ...).
+ * Like the reference, Pinhole and RadTan also run validate_params here
+ * (pinhole.rs:80, rad_tan.rs:135): a failure returns ACM_ERR_INVALID_PARAMS.*/
+ACM_API int acm_camera_init(acm_camera *cam, int model, const double *params,
+                            size_t num_params, uint32_t width, uint32_t height);
+
+/* validate_params (mod.rs:362-371 + per-model rules, e.g.
+ * double_sphere.rs:592-607).  Returns an acm_validation code. */
+ACM_API int acm_validate_params(const acm_camera *cam);
+
+/* Batched CameraModel::project (+ optional dense parameter Jacobian).
+ * points_3d: 3N f64 (layout), points_2d: 2N f64 out, status: N u8 out,
+ * jacobian: 2N*P f64 out or NULL.  Failed points: uv = NaN, J = 0.
+ * Replaces mod.rs:256 (per point) and the factor's Jacobian. */
+ACM_API int acm_project(const acm_camera *cam, size_t n,
+                        const double *points_3d, int layout, double *points_2d,
+                        uint8_t *status, double *jacobian, void *stream);
+
+/* Batched CameraModel::unproject (mod.rs:271).  rays: 3N f64 out written in
+ * `layout`; failed points: ray = NaN. */
+ACM_API int acm_unproject(const acm_camera *cam, size_t n,
+                          const double *points_2d, double *rays, int layout,
+                          uint8_t *status, void *stream);
+
+/* Factor linearisation: residual r = project(p_i) - obs_i (2N) and the
+ * 2N x P Jacobian (nullable) of *CameraParamsFactor
+ * (camera_converter.rs:378 & co).  status nullable. */
+ACM_API int acm_residual_jacobian(const acm_camera *cam, size_t n,
+                                  const double *points_3d, int layout,
+                                  const double *points_2d_obs,
+                                  int invalid_policy, double *residual,
+                                  double *jacobian, uint8_t *status,
+                                  void *stream);
+
+/* Fused LM linearisation: JtJ (P x P, row-major, symmetric), Jtr (P),
+ * cost = 0.5*sum ||r||^2 and n_valid, without materialising r or J.
+ * result (device, f64): [JtJ (P*P) | Jtr (P) | cost | n_valid].
+ * Deterministic: fixed per-block partials + an ordered final sum.  The
+ * workspace (device) must hold acm_normal_equations_workspace_size bytes. */
+ACM_API size_t acm_normal_equations_workspace_size(int model, size_t n);
+ACM_API int acm_normal_equations(const acm_camera *cam, size_t n,
+                                 const double *points_3d, int layout,
+                                 const double *points_2d_obs,
+                                 int invalid_policy, double *result,
+                                 void *workspace, size_t workspace_bytes,
+                                 void *stream);
+
+/* compute_reprojection_error (error_metrics.rs:62-121) minus the median:
+ * result (device, f64): [rmse, min, max, mean, stddev, n_valid, sum, sumsq]
+ * errors (nullable, device, N f64): per-point ||proj - obs||, NaN if failed.
+ * The stddev uses the reference's two-pass sum((e - mean)^2) / n. */
+ACM_API size_t acm_reprojection_stats_workspace_size(size_t n);
+ACM_API int acm_reprojection_stats(const acm_camera *cam, size_t n,
+                                   const double *points_3d, int layout,
+                                   const double *points_2d, double *result,
+                                   double *errors, void *workspace,
+                                   size_t workspace_bytes, void *stream);
+
+/* Exact median of the non-NaN values of `values` (the per-point errors of
+ * acm_reprojection_stats), error_metrics.rs:103-111: the mean of ranks
+ * m/2-1 and m/2 for even m, rank m/2 for odd m, m = n_valid (read from
+ * device memory n_valid_device if non-NULL, e.g. result[5] of
+ * acm_reprojection_stats, else the host value n_valid).  Values must be
+ * >= 0 or NaN.  out: device f64. */
+ACM_API size_t acm_median_workspace_size(size_t n);
+ACM_API int acm_median_valid(size_t n, const double *values,
+                             const double *n_valid_device, uint64_t n_valid,
+                             double *out, void *workspace,
+                             size_t workspace_bytes, void *stream);
+
+/* util::sample_points (point_sampling.rs:46-120): a grid of
+ * round(sqrt(n*w/h)) x round(sqrt(n*h/w)) cell centres (row-major, as the
+ * reference loop), each unprojected; a cell is kept iff the unprojection
+ * succeeds and ray.z > 0, in grid order (order-preserving compaction, so
+ * indices match the reference's Vec::push order).
+ * acm_sample_points_grid (host) gives the grid; the output buffers must hold
+ * ncx*ncy points (points_2d_out 2*cap f64, points_3d_out 3*cap f64 AoS).
+ * counts (device, 2 x uint64): [kept, ncx*ncy]. */
+ACM_API int acm_sample_points_grid(uint32_t width, uint32_t height, size_t n_requested,
+                                   uint32_t *num_cells_x, uint32_t *num_cells_y);
+ACM_API size_t acm_sample_points_workspace_size(const acm_camera *cam, size_t n_requested);
+ACM_API int acm_sample_points(const acm_camera *cam, size_t n_requested,
+                              double *points_2d_out, double *points_3d_out,
+                              uint64_t *counts, void *workspace,
+                              size_t workspace_bytes, void *stream);
+
+/* Diagnostics: last HIP error code / message of the calling thread. */
+ACM_API int acm_last_hip_error(void);
+ACM_API const char *acm_last_error(void);
+ACM_API const char *acm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACM_H */

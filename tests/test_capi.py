@@ -1,0 +1,118 @@
+"""CPU-side checks of the drop-in boundary (no GPU needed): libacm.so builds,
+loads, exports every ACM_API symbol declared in include/acm.h, and its host
+logic (parameter counts, XModel::new / validate_params semantics, argument
+validation, sample grid) mirrors the reference."""
+import ctypes
+import math
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    text = open(os.path.join(ROOT, "include", "acm.h")).read()
+    return sorted(set(re.findall(r"ACM_API\s+[\w\s\*]+?\b(acm_\w+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    from apex_camera_models import _lib
+    L = _lib.load()
+    syms = _header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_lib.EXPORTED_SYMBOLS)
+    assert b"gfx950" in L.acm_version()
+
+
+def test_num_params():
+    from apex_camera_models import _lib
+    L = _lib.load()
+    assert [L.acm_num_params(m) for m in range(7)] == [4, 9, 8, 6, 5, 6, 5]
+    assert L.acm_num_params(7) == -1
+
+
+def _init(model, params, w=752, h=480):
+    from apex_camera_models import _lib
+    cam = _lib.AcmCamera()
+    arr = (ctypes.c_double * max(len(params), 1))(*params)
+    rc = _lib.load().acm_camera_init(ctypes.byref(cam), model, arr, len(params), w, h)
+    return rc, cam
+
+
+def test_camera_init_param_count_errors():
+    # tests/model_conversions.rs:162-169: wrong parameter counts -> InvalidParams
+    from apex_camera_models import _lib
+    for model, n in [(3, 2), (2, 1), (1, 2), (4, 1), (5, 1), (0, 1)]:
+        rc, _ = _init(model, [500.0] * n)
+        assert rc == _lib.ERR_INVALID_PARAMS
+    assert "Expected" in _lib.last_error()
+    rc, cam = _init(2, [1.0] * 8)
+    assert rc == 0 and cam.num_params == 8 and cam.width == 752
+
+
+def test_camera_init_validates_pinhole_like_reference():
+    # tests/model_conversions.rs:172-186 (PinholeModel::new runs validate_params)
+    from apex_camera_models import _lib
+    for p in ([-500.0, 500.0, 320.0, 240.0], [0.0, 500.0, 320.0, 240.0],
+              [500.0, 500.0, math.inf, 240.0], [500.0, 500.0, 320.0, math.nan]):
+        rc, _ = _init(0, p)
+        assert rc == _lib.ERR_INVALID_PARAMS
+
+
+def test_validate_params_codes():
+    from apex_camera_models import _lib
+    L = _lib.load()
+    _, cam = _init(3, [350.0, 350.0, 320.0, 240.0, 0.58, -0.18])
+    assert L.acm_validate_params(ctypes.byref(cam)) == 0
+    cam.params[4] = 0.0  # double_sphere.rs:811-829: alpha must be in (0, 1]
+    assert L.acm_validate_params(ctypes.byref(cam)) == 6
+    cam.params[4] = 0.5
+    cam.params[5] = math.nan  # xi must be finite
+    assert L.acm_validate_params(ctypes.byref(cam)) == 6
+    cam.params[5] = 0.1
+    cam.params[0] = 0.0  # FocalLengthMustBePositive
+    assert L.acm_validate_params(ctypes.byref(cam)) == 4
+
+
+def test_argument_validation_before_any_launch():
+    from apex_camera_models import _lib
+    L = _lib.load()
+    _, cam = _init(2, [1.0] * 8)
+    # n == 0 is a no-op success (empty batch), bad layout / model rejected
+    assert L.acm_project(ctypes.byref(cam), 0, None, 0, None, None, None, None) == 0
+    assert L.acm_project(ctypes.byref(cam), 10, None, 0, None, None, None, None) == \
+        _lib.ERR_INVALID_ARGUMENT
+    assert L.acm_project(ctypes.byref(cam), 0, None, 7, None, None, None, None) == \
+        _lib.ERR_INVALID_ARGUMENT
+    cam.model = 42
+    assert L.acm_project(ctypes.byref(cam), 0, None, 0, None, None, None, None) == \
+        _lib.ERR_INVALID_MODEL
+    _, cam = _init(3, [350.0, 350.0, 320.0, 240.0, 0.58, -0.18])
+    assert L.acm_normal_equations(ctypes.byref(cam), 100, 1, 0, 1, 0, 1, 1, 8, None) == \
+        _lib.ERR_WORKSPACE_TOO_SMALL
+    assert L.acm_residual_jacobian(ctypes.byref(cam), 1, 1, 0, 1, 5, 1, None, None, None) == \
+        _lib.ERR_INVALID_ARGUMENT
+
+
+@pytest.mark.parametrize("w,h,n", [(752, 480, 100), (512, 512, 100_000_000), (752, 480, 500),
+                                   (752, 480, 2), (640, 480, 1)])
+def test_sample_grid_matches_reference_formula(w, h, n):
+    # point_sampling.rs:53-54: round(sqrt(n * w/h)) x round(sqrt(n * h/w))
+    from apex_camera_models import _lib
+    ncx, ncy = ctypes.c_uint32(), ctypes.c_uint32()
+    assert _lib.load().acm_sample_points_grid(w, h, n, ctypes.byref(ncx), ctypes.byref(ncy)) == 0
+    assert ncx.value == int(round(math.sqrt(n * (w / h))))
+    assert ncy.value == int(round(math.sqrt(n * (h / w))))
+
+
+def test_workspace_sizes():
+    from apex_camera_models import _lib
+    L = _lib.load()
+    K = 8 * 9 // 2 + 8 + 2
+    assert L.acm_normal_equations_workspace_size(2, 10_000_000) == (1024 + 1) * K * 8
+    assert L.acm_reprojection_stats_workspace_size(1000) >= 1000 * 8
+    assert L.acm_median_workspace_size(10) > 0
