@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "acm_sample_points_grid",
     "acm_sample_points_workspace_size",
     "acm_sample_points",
+    "acm_set_tuning",
     "acm_last_hip_error",
     "acm_last_error",
     "acm_version",
@@ -120,6 +121,8 @@ def load():
     L.acm_median_workspace_size.restype = sz
     L.acm_median_valid.argtypes = [sz, vp, vp, ctypes.c_uint64, vp, vp, sz, vp]
     L.acm_median_valid.restype = i
+    L.acm_set_tuning.argtypes = [i, i]
+    L.acm_set_tuning.restype = i
     L.acm_last_hip_error.argtypes = []
     L.acm_last_hip_error.restype = i
     L.acm_last_error.argtypes = []

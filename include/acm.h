@@ -203,6 +203,14 @@ ACM_API int acm_sample_points(const acm_camera *cam, size_t n_requested,
                               uint64_t *counts, void *workspace,
                               size_t workspace_bytes, void *stream);
 
+/* Process-wide kernel tuning knob (benchmark sweeps; results are identical
+ * for every setting).  ACM_TUNE_PROJECT_VARIANT: bit flags of acm_project's
+ * kernel, 1 = non-temporal stores, 2 = persistent grid-stride launch,
+ * 4 = two points per lane; -1 (default) = auto (non-temporal stores when the
+ * outputs exceed 256 MiB).  Returns the previous value or an error. */
+enum { ACM_TUNE_PROJECT_VARIANT = 0 };
+ACM_API int acm_set_tuning(int key, int value);
+
 /* Diagnostics: last HIP error code / message of the calling thread. */
 ACM_API int acm_last_hip_error(void);
 ACM_API const char *acm_last_error(void);
