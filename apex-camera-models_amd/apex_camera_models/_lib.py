@@ -59,6 +59,12 @@ EXPORTED_SYMBOLS = (
     "acm_sample_points_grid",
     "acm_sample_points_workspace_size",
     "acm_sample_points",
+    "acm_set_device",
+    "acm_device_malloc",
+    "acm_device_free",
+    "acm_memcpy_htod",
+    "acm_memcpy_dtoh",
+    "acm_stream_synchronize",
     "acm_set_tuning",
     "acm_last_hip_error",
     "acm_last_error",
@@ -121,6 +127,18 @@ def load():
     L.acm_median_workspace_size.restype = sz
     L.acm_median_valid.argtypes = [sz, vp, vp, ctypes.c_uint64, vp, vp, sz, vp]
     L.acm_median_valid.restype = i
+    L.acm_set_device.argtypes = [i]
+    L.acm_set_device.restype = i
+    L.acm_device_malloc.argtypes = [ctypes.POINTER(vp), sz]
+    L.acm_device_malloc.restype = i
+    L.acm_device_free.argtypes = [vp]
+    L.acm_device_free.restype = i
+    L.acm_memcpy_htod.argtypes = [vp, vp, sz, vp]
+    L.acm_memcpy_htod.restype = i
+    L.acm_memcpy_dtoh.argtypes = [vp, vp, sz, vp]
+    L.acm_memcpy_dtoh.restype = i
+    L.acm_stream_synchronize.argtypes = [vp]
+    L.acm_stream_synchronize.restype = i
     L.acm_set_tuning.argtypes = [i, i]
     L.acm_set_tuning.restype = i
     L.acm_last_hip_error.argtypes = []

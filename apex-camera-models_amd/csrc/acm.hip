@@ -985,6 +985,35 @@ ACM_API int acm_median_valid(size_t n, const double* values, const double* n_val
     return check_launch("acm_median_valid");
 }
 
+static int hip_rc(hipError_t e, const char* what) {
+    if (e == hipSuccess) return ACM_SUCCESS;
+    g_last_hip_error = (int)e;
+    return fail(ACM_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+ACM_API int acm_set_device(int device) { return hip_rc(hipSetDevice(device), "hipSetDevice"); }
+
+ACM_API int acm_device_malloc(void** ptr, size_t bytes) {
+    if (!ptr) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL argument");
+    return hip_rc(hipMalloc(ptr, bytes), "hipMalloc");
+}
+
+ACM_API int acm_device_free(void* ptr) { return hip_rc(hipFree(ptr), "hipFree"); }
+
+ACM_API int acm_memcpy_htod(void* dst, const void* src, size_t bytes, void* stream) {
+    return hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream),
+                  "hipMemcpyAsync(H2D)");
+}
+
+ACM_API int acm_memcpy_dtoh(void* dst, const void* src, size_t bytes, void* stream) {
+    return hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream),
+                  "hipMemcpyAsync(D2H)");
+}
+
+ACM_API int acm_stream_synchronize(void* stream) {
+    return hip_rc(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+}
+
 ACM_API int acm_set_tuning(int key, int value) {
     if (key == ACM_TUNE_PROJECT_VARIANT) {
         if (value < -1 || value > 5)

@@ -203,6 +203,16 @@ ACM_API int acm_sample_points(const acm_camera *cam, size_t n_requested,
                               uint64_t *counts, void *workspace,
                               size_t workspace_bytes, void *stream);
 
+/* Device-memory helpers so a host without HIP bindings (e.g. the Rust crate
+ * through `extern "C"`) can own device buffers: thin wrappers over
+ * hipMalloc / hipFree / hipMemcpyAsync / hipStreamSynchronize / hipSetDevice. */
+ACM_API int acm_set_device(int device);
+ACM_API int acm_device_malloc(void **ptr, size_t bytes);
+ACM_API int acm_device_free(void *ptr);
+ACM_API int acm_memcpy_htod(void *dst_device, const void *src_host, size_t bytes, void *stream);
+ACM_API int acm_memcpy_dtoh(void *dst_host, const void *src_device, size_t bytes, void *stream);
+ACM_API int acm_stream_synchronize(void *stream);
+
 /* Process-wide kernel tuning knob (benchmark sweeps; results are identical
  * for every setting).  ACM_TUNE_PROJECT_VARIANT: bit flags of acm_project's
  * kernel, 1 = non-temporal stores, 2 = persistent grid-stride launch,
