@@ -33,6 +33,40 @@ ERR_HIP = -4
 ERR_WORKSPACE_TOO_SMALL = -5
 
 
+class LmConfig(ctypes.Structure):
+    _fields_ = [
+        ("max_iterations", ctypes.c_int32),
+        ("invalid_policy", ctypes.c_int32),
+        ("cost_tolerance", ctypes.c_double),
+        ("parameter_tolerance", ctypes.c_double),
+        ("gradient_tolerance", ctypes.c_double),
+        ("initial_damping", ctypes.c_double),
+        ("has_bounds", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("lower", ctypes.c_double * 9),
+        ("upper", ctypes.c_double * 9),
+    ]
+
+
+class LmSummary(ctypes.Structure):
+    _fields_ = [
+        ("iterations", ctypes.c_int32),
+        ("termination", ctypes.c_int32),
+        ("evaluations", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("initial_cost", ctypes.c_double),
+        ("final_cost", ctypes.c_double),
+        ("n_valid", ctypes.c_double),
+    ]
+
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.c_void_p)
+ERR_NUMERICAL = -7
+LM_TERMINATION = {0: "MaxIterations", 1: "CostTolerance", 2: "ParameterTolerance",
+                  3: "GradientTolerance", 4: "Failed"}
+
+
 class AcmCamera(ctypes.Structure):
     _fields_ = [
         ("model", ctypes.c_int32),
@@ -54,11 +88,20 @@ EXPORTED_SYMBOLS = (
     "acm_normal_equations",
     "acm_reprojection_stats_workspace_size",
     "acm_reprojection_stats",
+    "acm_linear_system_columns",
+    "acm_linear_system_qr_workspace_size",
+    "acm_linear_system_qr",
+    "acm_linear_estimation_workspace_size",
+    "acm_linear_estimation",
+    "acm_lm_default_config",
+    "acm_lm_workspace_size",
+    "acm_lm_optimize",
     "acm_median_workspace_size",
     "acm_median_valid",
     "acm_sample_points_grid",
     "acm_sample_points_workspace_size",
     "acm_sample_points",
+    "acm_sample_points_range",
     "acm_set_device",
     "acm_device_malloc",
     "acm_device_free",
@@ -123,6 +166,25 @@ def load():
     L.acm_sample_points_workspace_size.restype = sz
     L.acm_sample_points.argtypes = [cam_p, sz, vp, vp, vp, vp, sz, vp]
     L.acm_sample_points.restype = i
+    L.acm_sample_points_range.argtypes = [cam_p, sz, sz, sz, vp, vp, vp, vp, sz, vp]
+    L.acm_sample_points_range.restype = i
+    L.acm_linear_system_columns.argtypes = [i]
+    L.acm_linear_system_columns.restype = i
+    L.acm_linear_system_qr_workspace_size.argtypes = [i, sz]
+    L.acm_linear_system_qr_workspace_size.restype = sz
+    L.acm_linear_system_qr.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp, sz, vp]
+    L.acm_linear_system_qr.restype = i
+    L.acm_linear_estimation_workspace_size.argtypes = [i, sz]
+    L.acm_linear_estimation_workspace_size.restype = sz
+    L.acm_linear_estimation.argtypes = [cam_p, sz, vp, i, vp, vp, sz, vp]
+    L.acm_linear_estimation.restype = i
+    L.acm_lm_default_config.argtypes = [ctypes.POINTER(LmConfig)]
+    L.acm_lm_default_config.restype = None
+    L.acm_lm_workspace_size.argtypes = [i, sz]
+    L.acm_lm_workspace_size.restype = sz
+    L.acm_lm_optimize.argtypes = [cam_p, sz, vp, i, vp, ctypes.POINTER(LmConfig), ALLREDUCE_FN,
+                                  vp, ctypes.POINTER(LmSummary), vp, sz, vp]
+    L.acm_lm_optimize.restype = i
     L.acm_median_workspace_size.argtypes = [sz]
     L.acm_median_workspace_size.restype = sz
     L.acm_median_valid.argtypes = [sz, vp, vp, ctypes.c_uint64, vp, vp, sz, vp]

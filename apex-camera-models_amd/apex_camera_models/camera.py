@@ -246,6 +246,36 @@ class CameraModel:
                                               _stream_handle()))
         return rays, st
 
+    # --- linear_estimation (GPU TSQR + host k x k SVD solve) ---------------
+    def linear_estimation(self, points_3d, points_2d) -> None:
+        """`XModel::linear_estimation(&Matrix3xX, &Matrix2xX)` (kannala_brandt.rs:164-272,
+        double_sphere.rs:225-290, ucm.rs:200-258, eucm.rs:216-288, rad_tan.rs:153-234).
+        Updates the distortion parameters in place; raises InvalidParams /
+        NumericalError like the reference."""
+        L = _lib.load()
+        p3 = _as_device_f64(points_3d, 3)
+        p2 = _as_device_f64(points_2d, 2)
+        if p3.shape[0] != p2.shape[0]:
+            raise InvalidParams("Number of 2D and 3D points must match")
+        n = p3.shape[0]
+        ws_bytes = L.acm_linear_estimation_workspace_size(self.MODEL_ID, n)
+        if ws_bytes == 0:
+            raise InvalidParams(f"{self.NAME} has no GPU linear_estimation")
+        ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=p3.device)
+        cam = self.acm_camera()
+        rc = L.acm_linear_estimation(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
+                                     p2.data_ptr(), ws.data_ptr(), ws_bytes, _stream_handle())
+        if rc == _lib.ERR_INVALID_PARAMS:
+            raise InvalidParams(_lib.last_error())
+        if rc == _lib.ERR_NUMERICAL:
+            raise NumericalError(_lib.last_error())
+        _lib.check(rc)
+        self._set_params(list(cam.params)[: self.NUM_PARAMS])
+
+    def _set_params(self, p: List[float]) -> None:
+        upd = self._from_params(p, self.resolution)
+        self.__dict__.update({k: v for k, v in upd.__dict__.items() if k != "resolution"})
+
     # --- per-point reference surface --------------------------------------
     def project(self, point_3d):
         """`fn project(&self, &Vector3) -> Result<Vector2, CameraModelError>`."""

@@ -1,0 +1,88 @@
+"""Model conversion pipeline of bin/camera_converter.rs (convert_to_*,
+:355-1163): sample correspondences from the input model, initialise the
+target, linear estimation, bounded LM, reprojection errors -- all on the GPU
+through libacm.so.  Report formatting, validation tables and image-quality
+metrics (reporting.rs, validation.rs, image_quality.rs) are out of scope."""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+
+from . import util
+from .camera import (CameraModel, DoubleSphereModel, EucmModel, Intrinsics, KannalaBrandtModel,
+                     RadTanModel, UcmModel)
+from .optimizer import CONVERTER_BOUNDS, LevenbergMarquardt, LevenbergMarquardtConfig
+
+
+@dataclass
+class ConversionMetrics:
+    model: CameraModel
+    model_name: str
+    final_reprojection_error: util.ProjectionError
+    initial_reprojection_error: util.ProjectionError
+    optimization_time_ms: float
+    convergence_status: str
+    lm_iterations: int = 0
+    lm_termination: str = ""
+
+
+# initial target parameters (camera_converter.rs:364-369, :500-505, :639-644,
+# :781-785, :911-916)
+def _init_target(name, src: CameraModel):
+    i = src.get_intrinsics()
+    res = src.get_resolution()
+    intr = Intrinsics(i.fx, i.fy, i.cx, i.cy)
+    if name == "double_sphere":
+        return DoubleSphereModel(intr, res, 0.5, 0.1)
+    if name == "kannala_brandt":
+        return KannalaBrandtModel(intr, res, [0.0] * 4)
+    if name == "rad_tan":
+        return RadTanModel(intr, res, [0.0] * 5)
+    if name == "ucm":
+        return UcmModel(intr, res, 0.5)
+    if name == "eucm":
+        return EucmModel(intr, res, 0.5, 1.0)
+    raise ValueError(name)
+
+
+DISPLAY = {"double_sphere": "Double Sphere", "kannala_brandt": "Kannala-Brandt",
+           "rad_tan": "Radial-Tangential", "ucm": "Unified Camera Model",
+           "eucm": "Extended Unified Camera Model"}
+
+
+def convert(input_model: CameraModel, target: str, points_3d, points_2d,
+            config: LevenbergMarquardtConfig = None, allreduce=None) -> ConversionMetrics:
+    """One `convert_to_<target>` (e.g. convert_to_double_sphere :355-488)."""
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    model = _init_target(target, input_model)
+    initial = util.compute_reprojection_error(model, points_3d, points_2d)
+    model.linear_estimation(points_3d, points_2d)
+    cfg = config or LevenbergMarquardtConfig()
+    status = "Converged"
+    res = None
+    try:
+        res = LevenbergMarquardt(cfg).optimize(model, points_3d, points_2d,
+                                               bounds=CONVERTER_BOUNDS[target],
+                                               allreduce=allreduce)
+        if res.termination == "Failed":
+            status = "Linear Only"
+    except Exception:  # camera_converter.rs:443: Err(_) => "Linear Only"
+        status = "Linear Only"
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    final = util.compute_reprojection_error(model, points_3d, points_2d)
+    return ConversionMetrics(model=model, model_name=DISPLAY[target],
+                             final_reprojection_error=final, initial_reprojection_error=initial,
+                             optimization_time_ms=ms, convergence_status=status,
+                             lm_iterations=res.iterations if res else 0,
+                             lm_termination=res.termination if res else "")
+
+
+def convert_all(input_model: CameraModel, num_points: int = 500,
+                targets=("double_sphere", "kannala_brandt", "rad_tan", "ucm", "eucm")):
+    """camera_converter.rs main (:127-350): sample_points once (:189), then
+    every target conversion."""
+    points_2d, points_3d = util.sample_points(input_model, num_points)
+    return {t: convert(input_model, t, points_3d, points_2d) for t in targets}

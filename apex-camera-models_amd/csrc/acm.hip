@@ -35,6 +35,8 @@ static int fail(int code, const std::string& msg) {
     return code;
 }
 
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+
 static int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -476,6 +478,7 @@ __global__ void k_reproj_final(const double* __restrict__ tot, const double* __r
 struct Grid {
     uint32_t ncx, ncy;
     double cw, ch;
+    size_t cell0;  // first cell of this launch (row-range shards, see acm_sample_points_range)
 };
 
 template <class TagT>
@@ -483,6 +486,7 @@ __device__ __forceinline__ bool sample_cell(const Cam<double>& c, const Grid& g,
                                             double& u, double& v, double& X, double& Y,
                                             double& Z) {
     using M = typename TagT::template type<double>;
+    cell += g.cell0;
     const uint32_t i = (uint32_t)(cell / g.ncx), j = (uint32_t)(cell % g.ncx);
     u = ((double)j + 0.5) * g.cw;  // :69
     v = ((double)i + 0.5) * g.ch;  // :70
@@ -633,6 +637,213 @@ __global__ void k_sel_finish(const SelState* __restrict__ a, const SelState* __r
     const double vb = __longlong_as_double((long long)b->prefix);
     if (m == 0) out[0] = __builtin_nan("");
     else out[0] = (m % 2 == 0) ? (va + vb) / 2.0 : vb;
+}
+
+// ------------------------------------------------------ linear estimation
+// The reference assembles A (2N x k) and b (2N) per point and solves with
+// nalgebra's SVD (kannala_brandt.rs:164-272, double_sphere.rs:225-290,
+// ucm.rs:200-258, eucm.rs:216-288, rad_tan.rs:153-234).  At 1e8
+// correspondences A alone is 1.6-6.4 GB, so here it is never written: a
+// tall-skinny QR (TSQR) folds each row of [A | b] into a per-lane upper-
+// triangular R ((k+1) x (k+1), Givens rotations), lanes merge their R's
+// through wave shuffles, waves through LDS, workgroups in a fixed-order
+// second pass.  A = QR gives the same singular values and least-squares
+// solution as the SVD of A (x = R_A^+ Q^T b), numerically stable (no normal
+// equations), and the reduction order is fixed -> bit-reproducible.
+template <int M>
+struct Tri {
+    static constexpr int S = M * (M + 1) / 2;
+    static __device__ __host__ constexpr int at(int r, int c) { return r * M - r * (r - 1) / 2 + (c - r); }
+};
+
+// fold one row (length M, entries before `first` are zero) into R
+template <int M>
+__device__ __forceinline__ void tri_add_row(double (&R)[Tri<M>::S], double (&row)[M]) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        const double b = row[j];
+        if (b != 0.0) {
+            const double a = R[Tri<M>::at(j, j)];
+            const double r = sqrt(a * a + b * b);
+            const double c = a / r, s = b / r;
+            R[Tri<M>::at(j, j)] = r;
+#pragma unroll
+            for (int l = j + 1; l < M; ++l) {
+                const double Rl = R[Tri<M>::at(j, l)], rl = row[l];
+                R[Tri<M>::at(j, l)] = c * Rl + s * rl;
+                row[l] = c * rl - s * Rl;
+            }
+        }
+    }
+}
+
+template <int M>
+__device__ __forceinline__ void tri_merge(double (&R)[Tri<M>::S], const double (&O)[Tri<M>::S]) {
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        double row[M];
+#pragma unroll
+        for (int c = 0; c < M; ++c) row[c] = c < r ? 0.0 : O[Tri<M>::at(r, c)];
+        tri_add_row<M>(R, row);
+    }
+}
+
+// Rows of [A | b] for point i (2 rows), per model; returns false to skip
+// the point, sets *err on the reference's NumericalError path.
+template <int MODEL>
+struct LinRows;
+
+template <>
+struct LinRows<ACM_KANNALA_BRANDT> {  // kannala_brandt.rs:184-259, k = 4
+    static constexpr int K = 4;
+    __device__ static bool rows(const Cam<double>& c, double X, double Y, double Z, double u,
+                                double v, double (&r0)[K + 1], double (&r1)[K + 1], int& err) {
+        const double fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        if (Z <= kEps) return false;  // :195-197
+        const double r = sqrt(X * X + Y * Y);
+        const double theta = atan2(r, Z);
+        const double t2 = theta * theta, t3 = t2 * theta, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
+        r0[0] = r1[0] = t3; r0[1] = r1[1] = t5; r0[2] = r1[2] = t7; r0[3] = r1[3] = t9;
+        const double x_r = r < kEps ? 0.0 : X / r;
+        const double y_r = r < kEps ? 0.0 : Y / r;
+        if ((fabs(fx * x_r) < kEps && fabs(x_r) > kEps) || (fabs(fy * y_r) < kEps && fabs(y_r) > kEps))
+            err = 1;  // :229-238
+        r0[K] = fabs(x_r) > kEps ? (u - cx) / (fx * x_r) - theta : (fabs(u - cx) < kEps ? -theta : 0.0);
+        r1[K] = fabs(y_r) > kEps ? (v - cy) / (fy * y_r) - theta : (fabs(v - cy) < kEps ? -theta : 0.0);
+        return true;
+    }
+};
+
+struct LinRowsAlpha {  // double_sphere.rs:242-258 (= ucm.rs, eucm.rs), k = 1
+    static constexpr int K = 1;
+    __device__ static bool rows(const Cam<double>& c, double X, double Y, double Z, double u,
+                                double v, double (&r0)[K + 1], double (&r1)[K + 1], int&) {
+        const double fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const double d = sqrt(X * X + Y * Y + Z * Z);
+        const double u_cx = u - cx, v_cy = v - cy;
+        r0[0] = u_cx * (d - Z);
+        r1[0] = v_cy * (d - Z);
+        r0[1] = (fx * X) - (u_cx * Z);
+        r1[1] = (fy * Y) - (v_cy * Z);
+        return true;
+    }
+};
+template <> struct LinRows<ACM_DOUBLE_SPHERE> : LinRowsAlpha {};
+template <> struct LinRows<ACM_UCM> : LinRowsAlpha {};
+template <> struct LinRows<ACM_EUCM> : LinRowsAlpha {};
+
+template <>
+struct LinRows<ACM_RADTAN> {  // rad_tan.rs:168-198, k = 3
+    static constexpr int K = 3;
+    __device__ static bool rows(const Cam<double>& c, double X, double Y, double Z, double u,
+                                double v, double (&r0)[K + 1], double (&r1)[K + 1], int&) {
+        const double fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const double xn = X / Z, yn = Y / Z;
+        const double r2 = xn * xn + yn * yn, r4 = r2 * r2, r6 = r4 * r2;
+        r0[0] = fx * xn * r2; r0[1] = fx * xn * r4; r0[2] = fx * xn * r6;
+        r1[0] = fy * yn * r2; r1[1] = fy * yn * r4; r1[2] = fy * yn * r6;
+        r0[3] = u - (fx * xn + cx);
+        r1[3] = v - (fy * yn + cy);
+        return true;
+    }
+};
+
+constexpr int kTsqrMaxBlocks = 1024;
+
+template <int MODEL, int LAYOUT>
+__global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
+                                                 const double* __restrict__ pts,
+                                                 const double* __restrict__ obs,
+                                                 double* __restrict__ parts,
+                                                 int* __restrict__ err_flag) {
+    using RW = LinRows<MODEL>;
+    constexpr int M = RW::K + 1;
+    constexpr int S = Tri<M>::S;
+    const Cam<double> c = make_cam<double>(cam);
+    double R[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) R[q] = 0.0;
+    int err = 0;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        double x, y, z;
+        load_point<LAYOUT>(pts, n, i, x, y, z);
+        const double2 o = *reinterpret_cast<const double2*>(obs + 2 * i);
+        double r0[M], r1[M];
+        if (RW::rows(c, x, y, z, o.x, o.y, r0, r1, err)) {
+            tri_add_row<M>(R, r0);
+            tri_add_row<M>(R, r1);
+        }
+    }
+    // wave merge (fixed butterfly order)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        double O[S];
+#pragma unroll
+        for (int q = 0; q < S; ++q) O[q] = __shfl_down(R[q], off, 64);
+        if ((threadIdx.x & 63) < off) tri_merge<M>(R, O);
+    }
+    __shared__ double sm[kBlock / 64][S];
+    __shared__ int serr;
+    if (threadIdx.x == 0) serr = 0;
+    __syncthreads();
+    if (err) atomicOr(&serr, 1);
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) sm[threadIdx.x >> 6][q] = R[q];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) {
+            double O[S];
+#pragma unroll
+            for (int q = 0; q < S; ++q) O[q] = sm[w][q];
+            tri_merge<M>(R, O);
+        }
+#pragma unroll
+        for (int q = 0; q < S; ++q) parts[(size_t)blockIdx.x * S + q] = R[q];
+        if (serr) atomicOr(err_flag, 1);
+    }
+}
+
+// fixed-order merge of the per-workgroup R factors: 256 lanes take strided
+// blocks, then the same butterfly + LDS order as above
+template <int M>
+__global__ __launch_bounds__(kBlock) void k_tsqr_final(const double* __restrict__ parts, int nb,
+                                                       double* __restrict__ out) {
+    constexpr int S = Tri<M>::S;
+    double R[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) R[q] = 0.0;
+    for (int b = threadIdx.x; b < nb; b += kBlock) {
+        double O[S];
+#pragma unroll
+        for (int q = 0; q < S; ++q) O[q] = parts[(size_t)b * S + q];
+        tri_merge<M>(R, O);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        double O[S];
+#pragma unroll
+        for (int q = 0; q < S; ++q) O[q] = __shfl_down(R[q], off, 64);
+        if ((threadIdx.x & 63) < off) tri_merge<M>(R, O);
+    }
+    __shared__ double sm[kBlock / 64][S];
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) sm[threadIdx.x >> 6][q] = R[q];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) {
+            double O[S];
+#pragma unroll
+            for (int q = 0; q < S; ++q) O[q] = sm[w][q];
+            tri_merge<M>(R, O);
+        }
+#pragma unroll
+        for (int q = 0; q < S; ++q) out[q] = R[q];
+    }
 }
 
 static unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -920,25 +1131,30 @@ ACM_API size_t acm_sample_points_workspace_size(const acm_camera* cam, size_t n_
     return 2 * nb * sizeof(uint64_t);
 }
 
-ACM_API int acm_sample_points(const acm_camera* cam, size_t n_requested, double* points_2d_out,
-                              double* points_3d_out, uint64_t* counts, void* workspace,
-                              size_t workspace_bytes, void* stream) {
+ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, size_t cell_begin,
+                                    size_t cell_end, double* points_2d_out, double* points_3d_out,
+                                    uint64_t* counts, void* workspace, size_t workspace_bytes,
+                                    void* stream) {
     int rc = check_cam(cam);
     if (rc) return rc;
     uint32_t ncx, ncy;
     if ((rc = acm_sample_points_grid(cam->width, cam->height, n_requested, &ncx, &ncy))) return rc;
+    const size_t total = (size_t)ncx * ncy;
+    if (cell_end > total) cell_end = total;
+    if (cell_begin > cell_end) return fail(ACM_ERR_INVALID_ARGUMENT, "cell_begin > cell_end");
     if (!points_2d_out || !points_3d_out || !counts || !workspace)
         return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
-    if (workspace_bytes < acm_sample_points_workspace_size(cam, n_requested))
+    const size_t cells = cell_end - cell_begin;
+    const size_t nb = cells ? (cells + kBlock - 1) / kBlock : 1;
+    if (workspace_bytes < 2 * nb * sizeof(uint64_t))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "sample_points workspace too small");
-    const size_t cells = (size_t)ncx * ncy;
-    const size_t nb = (cells + kBlock - 1) / kBlock;
     if (nb > 0x7fffffffull) return fail(ACM_ERR_INVALID_ARGUMENT, "sample grid too large");
     Grid g;
     g.ncx = ncx;
     g.ncy = ncy;
-    g.cw = (double)cam->width / (double)ncx;  // :57
+    g.cw = (double)cam->width / (double)ncx;  // point_sampling.rs:57
     g.ch = (double)cam->height / (double)ncy;
+    g.cell0 = cell_begin;
     uint64_t* cnt = (uint64_t*)workspace;
     uint64_t* off = cnt + nb;
     hipStream_t s = (hipStream_t)stream;
@@ -952,6 +1168,76 @@ ACM_API int acm_sample_points(const acm_camera* cam, size_t n_requested, double*
                            g, cells, off, points_2d_out, points_3d_out);
         return check_launch("acm_sample_points");
     });
+}
+
+ACM_API int acm_sample_points(const acm_camera* cam, size_t n_requested, double* points_2d_out,
+                              double* points_3d_out, uint64_t* counts, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+    return acm_sample_points_range(cam, n_requested, 0, ~(size_t)0, points_2d_out, points_3d_out,
+                                   counts, workspace, workspace_bytes, stream);
+}
+
+ACM_API int acm_linear_system_columns(int model) {
+    switch (model) {
+    case ACM_KANNALA_BRANDT: return 4;
+    case ACM_RADTAN: return 3;
+    case ACM_DOUBLE_SPHERE:
+    case ACM_UCM:
+    case ACM_EUCM: return 1;
+    default: return -1;
+    }
+}
+
+static size_t tsqr_blocks(size_t n) {
+    size_t nb = (n + kBlock - 1) / kBlock;
+    if (nb > (size_t)kTsqrMaxBlocks) nb = kTsqrMaxBlocks;
+    return nb ? nb : 1;
+}
+
+ACM_API size_t acm_linear_system_qr_workspace_size(int model, size_t n) {
+    const int k = acm_linear_system_columns(model);
+    if (k < 0) return 0;
+    const int M = k + 1, S = M * (M + 1) / 2;
+    return tsqr_blocks(n) * S * sizeof(double);
+}
+
+ACM_API int acm_linear_system_qr(const acm_camera* cam, size_t n, const double* points_3d,
+                                 int layout, const double* points_2d, double* r_factor,
+                                 int* error_flag, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if ((rc = check_layout(layout))) return rc;
+    const int k = acm_linear_system_columns(cam->model);
+    if (k < 0) return fail(ACM_ERR_NOT_SUPPORTED, "model has no linear_estimation");
+    if (!r_factor || !error_flag || !workspace || (n && (!points_3d || !points_2d)))
+        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_linear_system_qr_workspace_size(cam->model, n))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "linear-system workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = (int)tsqr_blocks(n);
+    double* parts = (double*)workspace;
+    if (hipMemsetAsync(error_flag, 0, sizeof(int), s) != hipSuccess)
+        return check_launch("acm_linear_system_qr (memset)");
+    auto go = [&](auto model_c) {
+        constexpr int MOD = decltype(model_c)::value;
+        constexpr int M = LinRows<MOD>::K + 1;
+        if (layout == ACM_LAYOUT_AOS)
+            hipLaunchKernelGGL((k_tsqr<MOD, ACM_LAYOUT_AOS>), dim3(nb), dim3(kBlock), 0, s, *cam,
+                               n, points_3d, points_2d, parts, error_flag);
+        else
+            hipLaunchKernelGGL((k_tsqr<MOD, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s, *cam,
+                               n, points_3d, points_2d, parts, error_flag);
+        hipLaunchKernelGGL((k_tsqr_final<M>), dim3(1), dim3(kBlock), 0, s, parts, nb, r_factor);
+    };
+    switch (cam->model) {
+    case ACM_KANNALA_BRANDT: go(std::integral_constant<int, ACM_KANNALA_BRANDT>{}); break;
+    case ACM_RADTAN: go(std::integral_constant<int, ACM_RADTAN>{}); break;
+    case ACM_DOUBLE_SPHERE: go(std::integral_constant<int, ACM_DOUBLE_SPHERE>{}); break;
+    case ACM_UCM: go(std::integral_constant<int, ACM_UCM>{}); break;
+    default: go(std::integral_constant<int, ACM_EUCM>{}); break;
+    }
+    return check_launch("acm_linear_system_qr");
 }
 
 ACM_API size_t acm_median_workspace_size(size_t n) {
@@ -984,6 +1270,7 @@ ACM_API int acm_median_valid(size_t n, const double* values, const double* n_val
                        (unsigned long long)n_valid, out);
     return check_launch("acm_median_valid");
 }
+
 
 static int hip_rc(hipError_t e, const char* what) {
     if (e == hipSuccess) return ACM_SUCCESS;

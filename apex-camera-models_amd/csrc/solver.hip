@@ -1,0 +1,351 @@
+// solver.hip -- host-side drivers on top of the kernels: linear_estimation
+// (TSQR factor from the GPU, k x k SVD solve on the host) and the
+// Levenberg-Marquardt loop of the model conversion (normal equations from
+// the fused GPU kernel, optional cross-rank all-reduce callback, P x P
+// Cholesky on the host).
+//
+// Reference: bin/camera_converter.rs:355-1163 (convert_to_*: linear
+// estimation then apex-solver LM with bounds and
+// max_iterations=100, cost_tolerance=1e-6, parameter_tolerance=1e-8,
+// gradient_tolerance=1e-6).  apex-solver 0.1.5's LM source is absent, so the
+// LM here is a standard bounded Levenberg-Marquardt (Madsen/Nielsen damping
+// update, Marquardt diagonal scaling, projection onto the bounds), with the
+// reference's configuration; DESIGN.md documents the (unpinned) choice.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "acm.h"
+
+namespace acm {
+int set_error(int code, const std::string& msg);  // acm.hip (one last-error slot)
+}
+
+namespace {
+
+int sfail(int code, const std::string& m) { return acm::set_error(code, m); }
+
+int hip_ok(hipError_t e) { return e == hipSuccess ? ACM_SUCCESS : ACM_ERR_HIP; }
+
+// One-sided Jacobi SVD of a k x k matrix A (row-major), then
+// x = V diag(1/s) U^T b with singular values <= eps treated as zero --
+// the semantics of nalgebra's SVD::solve(b, eps).
+void svd_solve(int k, const double* A, const double* b, double eps, double* x) {
+    std::vector<double> W(A, A + k * k), V(k * k, 0.0);
+    for (int i = 0; i < k; ++i) V[i * k + i] = 1.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < k; ++p)
+            for (int q = p + 1; q < k; ++q) {
+                double al = 0, be = 0, ga = 0;
+                for (int i = 0; i < k; ++i) {
+                    al += W[i * k + p] * W[i * k + p];
+                    be += W[i * k + q] * W[i * k + q];
+                    ga += W[i * k + p] * W[i * k + q];
+                }
+                if (ga == 0.0) continue;
+                off = std::fmax(off, std::fabs(ga) / std::sqrt(al * be));
+                const double zeta = (be - al) / (2.0 * ga);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (std::fabs(zeta) + std::sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / std::sqrt(1.0 + t * t), s = c * t;
+                for (int i = 0; i < k; ++i) {
+                    const double wp = W[i * k + p], wq = W[i * k + q];
+                    W[i * k + p] = c * wp - s * wq;
+                    W[i * k + q] = s * wp + c * wq;
+                    const double vp = V[i * k + p], vq = V[i * k + q];
+                    V[i * k + p] = c * vp - s * vq;
+                    V[i * k + q] = s * vp + c * vq;
+                }
+            }
+        if (off < 1e-15) break;
+    }
+    for (int i = 0; i < k; ++i) x[i] = 0.0;
+    for (int j = 0; j < k; ++j) {
+        double sj = 0.0;
+        for (int i = 0; i < k; ++i) sj += W[i * k + j] * W[i * k + j];
+        sj = std::sqrt(sj);
+        if (!(sj > eps)) continue;
+        double utb = 0.0;  // u_j = W[:, j] / s_j
+        for (int i = 0; i < k; ++i) utb += W[i * k + j] * b[i];
+        const double coef = utb / (sj * sj);
+        for (int i = 0; i < k; ++i) x[i] += V[i * k + j] * coef;
+    }
+}
+
+bool cholesky_solve(int P, const double* A, const double* b, double* x) {
+    double L[81];
+    for (int i = 0; i < P; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double s = A[i * P + j];
+            for (int q = 0; q < j; ++q) s -= L[i * P + q] * L[j * P + q];
+            if (i == j) {
+                if (!(s > 0.0)) return false;
+                L[i * P + i] = std::sqrt(s);
+            } else {
+                L[i * P + j] = s / L[j * P + j];
+            }
+        }
+    double y[9];
+    for (int i = 0; i < P; ++i) {
+        double s = b[i];
+        for (int q = 0; q < i; ++q) s -= L[i * P + q] * y[q];
+        y[i] = s / L[i * P + i];
+    }
+    for (int i = P - 1; i >= 0; --i) {
+        double s = y[i];
+        for (int q = i + 1; q < P; ++q) s -= L[q * P + i] * x[q];
+        x[i] = s / L[i * P + i];
+    }
+    return true;
+}
+
+int validate(const acm_camera* cam) {
+    const int v = acm_validate_params(cam);
+    if (v == ACM_VALID) return ACM_SUCCESS;
+    return sfail(ACM_ERR_INVALID_PARAMS, "validate_params failed after linear estimation");
+}
+
+}  // namespace
+
+extern "C" {
+
+ACM_API size_t acm_linear_estimation_workspace_size(int model, size_t n) {
+    const size_t qr = acm_linear_system_qr_workspace_size(model, n);
+    if (!qr) return 0;
+    return qr + 32 * sizeof(double);
+}
+
+// linear_estimation (kannala_brandt.rs:164-272, double_sphere.rs:225-290,
+// ucm.rs:200-258, eucm.rs:216-288, rad_tan.rs:153-234): updates cam->params.
+ACM_API int acm_linear_estimation(acm_camera* cam, size_t n, const double* points_3d, int layout,
+                                  const double* points_2d, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+    if (!cam) return sfail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
+    const int k = acm_linear_system_columns(cam->model);
+    if (k < 0) return sfail(ACM_ERR_NOT_SUPPORTED, "model has no linear_estimation");
+    if (cam->model == ACM_KANNALA_BRANDT && n < 4)  // :174-178
+        return sfail(ACM_ERR_INVALID_PARAMS, "Not enough points for linear estimation (need at least 4)");
+    if (cam->model == ACM_RADTAN && n < 3)  // rad_tan.rs:152-156
+        return sfail(ACM_ERR_INVALID_PARAMS, "Need at least 3 points for RadTan linear estimation");
+    if (cam->model == ACM_EUCM && n < 1)  // eucm.rs:228-232
+        return sfail(ACM_ERR_INVALID_PARAMS, "Need at least 1 point for EUCM linear estimation");
+    const size_t need = acm_linear_estimation_workspace_size(cam->model, n);
+    if (!workspace || workspace_bytes < need)
+        return sfail(ACM_ERR_WORKSPACE_TOO_SMALL, "linear-estimation workspace too small");
+    const int M = k + 1, S = M * (M + 1) / 2;
+    const size_t qr = acm_linear_system_qr_workspace_size(cam->model, n);
+    double* d_r = (double*)((char*)workspace + qr);
+    int* d_err = (int*)(d_r + 16);
+    int rc = acm_linear_system_qr(cam, n, points_3d, layout, points_2d, d_r, d_err, workspace, qr,
+                                  stream);
+    if (rc) return rc;
+    double R[16];
+    int err = 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (hip_ok(hipMemcpyAsync(R, d_r, S * sizeof(double), hipMemcpyDeviceToHost, s)) ||
+        hip_ok(hipMemcpyAsync(&err, d_err, sizeof(int), hipMemcpyDeviceToHost, s)) ||
+        hip_ok(hipStreamSynchronize(s)))
+        return sfail(ACM_ERR_HIP, "linear estimation: device copy failed");
+    if (err) return sfail(ACM_ERR_NUMERICAL, "fx * x_r is zero in linear estimation");
+    // R = [[R_A, z], [0, rho]] (packed upper triangle, row-major)
+    double RA[16] = {0}, z[4] = {0}, x[4] = {0};
+    auto at = [M](int r, int c) { return r * M - r * (r - 1) / 2 + (c - r); };
+    for (int r = 0; r < k; ++r) {
+        for (int c = r; c < k; ++c) RA[r * k + c] = R[at(r, c)];
+        z[r] = R[at(r, k)];
+    }
+    const double eps = cam->model == ACM_KANNALA_BRANDT ? 2.220446049250313e-16 : 1e-10;
+    svd_solve(k, RA, z, eps, x);
+    double* p = cam->params;
+    switch (cam->model) {
+    case ACM_KANNALA_BRANDT:  // :268-270
+        for (int i = 0; i < 4; ++i) p[4 + i] = x[i];
+        return validate(cam);
+    case ACM_DOUBLE_SPHERE:  // :269-287
+        p[4] = x[0];
+        p[5] = 0.0;
+        if (p[4] <= 0.0) p[4] = 0.01;
+        else if (p[4] > 1.0) p[4] = 1.0;
+        return validate(cam);
+    case ACM_UCM:  // ucm.rs:245-255
+        p[4] = x[0];
+        if (p[4] <= 0.0) p[4] = 0.01;
+        return validate(cam);
+    case ACM_EUCM:  // eucm.rs:234-285
+        p[5] = 1.0;
+        p[4] = x[0];
+        if (p[4] <= 0.0) p[4] = 0.01;
+        else if (p[4] > 2.0) p[4] = 2.0;
+        return validate(cam);
+    case ACM_RADTAN:  // rad_tan.rs:209-214
+        p[4] = x[0];
+        p[5] = x[1];
+        p[6] = 0.0;
+        p[7] = 0.0;
+        p[8] = x[2];
+        return ACM_SUCCESS;
+    default: return sfail(ACM_ERR_NOT_SUPPORTED, "unsupported model");
+    }
+}
+
+ACM_API void acm_lm_default_config(acm_lm_config* cfg) {
+    if (!cfg) return;
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->max_iterations = 100;  // camera_converter.rs:410-415
+    cfg->cost_tolerance = 1e-6;
+    cfg->parameter_tolerance = 1e-8;
+    cfg->gradient_tolerance = 1e-6;
+    cfg->initial_damping = 1e-4;
+    cfg->invalid_policy = ACM_INVALID_SKIP;
+    cfg->has_bounds = 0;
+    for (int i = 0; i < ACM_MAX_PARAMS; ++i) {
+        cfg->lower[i] = -INFINITY;
+        cfg->upper[i] = INFINITY;
+    }
+}
+
+ACM_API size_t acm_lm_workspace_size(int model, size_t n) {
+    const int P = acm_num_params(model);
+    if (P < 0) return 0;
+    return acm_normal_equations_workspace_size(model, n) + (size_t)(P * P + P + 2 + 8) * 8;
+}
+
+ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, int layout,
+                            const double* points_2d, const acm_lm_config* cfg,
+                            acm_allreduce_fn allreduce, void* allreduce_ctx,
+                            acm_lm_summary* summary, void* workspace, size_t workspace_bytes,
+                            void* stream) {
+    if (!cam || !cfg) return sfail(ACM_ERR_INVALID_ARGUMENT, "NULL argument");
+    const int P = acm_num_params(cam->model);
+    if (P < 0) return sfail(ACM_ERR_INVALID_MODEL, "unknown camera model id");
+    const size_t need = acm_lm_workspace_size(cam->model, n);
+    if (!workspace || workspace_bytes < need)
+        return sfail(ACM_ERR_WORKSPACE_TOO_SMALL, "LM workspace too small");
+    const size_t ne_ws = acm_normal_equations_workspace_size(cam->model, n);
+    double* d_res = (double*)((char*)workspace + ne_ws);
+    const int R = P * P + P + 2;
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<double> h(R);
+    acm_lm_summary sum;
+    std::memset(&sum, 0, sizeof(sum));
+
+    auto clamp = [&](double* x) {
+        if (!cfg->has_bounds) return;
+        for (int i = 0; i < P; ++i) x[i] = std::fmin(std::fmax(x[i], cfg->lower[i]), cfg->upper[i]);
+    };
+    // evaluate JtJ, Jtr, cost at parameter vector x
+    auto eval = [&](const double* x, double* A, double* g, double* F, double* nv) -> int {
+        acm_camera c = *cam;
+        for (int i = 0; i < P; ++i) c.params[i] = x[i];
+        int rc = acm_normal_equations(&c, n, points_3d, layout, points_2d, cfg->invalid_policy,
+                                      d_res, workspace, ne_ws, stream);
+        if (rc) return rc;
+        if (allreduce) {
+            rc = allreduce(allreduce_ctx, d_res, (size_t)R, stream);
+            if (rc) return sfail(ACM_ERR_HIP, "all-reduce callback failed");
+        }
+        if (hip_ok(hipMemcpyAsync(h.data(), d_res, R * sizeof(double), hipMemcpyDeviceToHost, s)) ||
+            hip_ok(hipStreamSynchronize(s)))
+            return sfail(ACM_ERR_HIP, "LM: device copy failed");
+        ++sum.evaluations;
+        std::memcpy(A, h.data(), P * P * sizeof(double));
+        for (int i = 0; i < P; ++i) g[i] = h[P * P + i];
+        *F = h[P * P + P];
+        *nv = h[P * P + P + 1];
+        return ACM_SUCCESS;
+    };
+
+    double x[9], A[81], g[9], F, nv;
+    for (int i = 0; i < P; ++i) x[i] = cam->params[i];
+    clamp(x);
+    int rc = eval(x, A, g, &F, &nv);
+    if (rc) return rc;
+    sum.initial_cost = F;
+    double dmax = 0.0;
+    for (int i = 0; i < P; ++i) dmax = std::fmax(dmax, A[i * P + i]);
+    double mu = cfg->initial_damping, nu = 2.0;
+    int term = ACM_LM_MAX_ITERATIONS;
+    auto ginf = [&](const double* gg) {
+        double m = 0.0;
+        for (int i = 0; i < P; ++i) m = std::fmax(m, std::fabs(gg[i]));
+        return m;
+    };
+    if (!std::isfinite(F)) term = ACM_LM_FAILED;
+    else if (ginf(g) <= cfg->gradient_tolerance) term = ACM_LM_GRADIENT;
+    int it = 0;
+    while (term == ACM_LM_MAX_ITERATIONS && it < cfg->max_iterations) {
+        ++it;
+        // (JtJ + mu * diag(JtJ)) h = -g   (Marquardt scaling, floored)
+        double Ad[81], mg[9], hstep[9];
+        for (int i = 0; i < P * P; ++i) Ad[i] = A[i];
+        for (int i = 0; i < P; ++i) {
+            Ad[i * P + i] += mu * std::fmax(A[i * P + i], 1e-12 * std::fmax(dmax, 1.0));
+            mg[i] = -g[i];
+        }
+        if (!cholesky_solve(P, Ad, mg, hstep)) {
+            mu *= nu;
+            nu *= 2.0;
+            continue;
+        }
+        double xn[9], xnorm = 0.0, hnorm = 0.0;
+        for (int i = 0; i < P; ++i) xn[i] = x[i] + hstep[i];
+        clamp(xn);
+        for (int i = 0; i < P; ++i) {
+            hstep[i] = xn[i] - x[i];
+            hnorm += hstep[i] * hstep[i];
+            xnorm += x[i] * x[i];
+        }
+        hnorm = std::sqrt(hnorm);
+        xnorm = std::sqrt(xnorm);
+        if (hnorm <= cfg->parameter_tolerance * (xnorm + cfg->parameter_tolerance)) {
+            term = ACM_LM_PARAMETER;
+            break;
+        }
+        double An[81], gn[9], Fn, nvn;
+        rc = eval(xn, An, gn, &Fn, &nvn);
+        if (rc) return rc;
+        // predicted reduction L(0) - L(h) = -(g.h + 0.5 h.A.h)
+        double gh = 0.0, hAh = 0.0;
+        for (int i = 0; i < P; ++i) {
+            gh += g[i] * hstep[i];
+            double t = 0.0;
+            for (int j = 0; j < P; ++j) t += A[i * P + j] * hstep[j];
+            hAh += hstep[i] * t;
+        }
+        const double pred = -(gh + 0.5 * hAh);
+        const double rho = (std::isfinite(Fn) && pred > 0.0) ? (F - Fn) / pred : -1.0;
+        if (rho > 0.0) {
+            const double dF = F - Fn;
+            const double Fold = F;
+            for (int i = 0; i < P; ++i) x[i] = xn[i];
+            std::memcpy(A, An, sizeof(double) * P * P);
+            std::memcpy(g, gn, sizeof(double) * P);
+            F = Fn;
+            nv = nvn;
+            const double t = 2.0 * rho - 1.0;
+            mu *= std::fmax(1.0 / 3.0, 1.0 - t * t * t);
+            nu = 2.0;
+            if (ginf(g) <= cfg->gradient_tolerance) term = ACM_LM_GRADIENT;
+            else if (dF <= cfg->cost_tolerance * Fold) term = ACM_LM_COST;
+        } else {
+            mu *= nu;
+            nu *= 2.0;
+            if (!std::isfinite(mu) || mu > 1e32) {
+                term = ACM_LM_FAILED;
+                break;
+            }
+        }
+    }
+    for (int i = 0; i < P; ++i) cam->params[i] = x[i];
+    sum.iterations = it;
+    sum.termination = term;
+    sum.final_cost = F;
+    sum.n_valid = nv;
+    if (summary) *summary = sum;
+    return ACM_SUCCESS;
+}
+
+}  // extern "C"

@@ -81,7 +81,8 @@ typedef enum acm_result {
     ACM_ERR_INVALID_ARGUMENT = -3,
     ACM_ERR_HIP = -4,
     ACM_ERR_WORKSPACE_TOO_SMALL = -5,
-    ACM_ERR_NOT_SUPPORTED = -6
+    ACM_ERR_NOT_SUPPORTED = -6,
+    ACM_ERR_NUMERICAL = -7 /* CameraModelError::NumericalError */
 } acm_result;
 
 typedef enum acm_validation {
@@ -175,6 +176,77 @@ ACM_API int acm_reprojection_stats(const acm_camera *cam, size_t n,
                                    double *errors, void *workspace,
                                    size_t workspace_bytes, void *stream);
 
+/* linear_estimation (kannala_brandt.rs:164-272, double_sphere.rs:225-290,
+ * ucm.rs:200-258, eucm.rs:216-288, rad_tan.rs:153-234).  The 2N x k system
+ * [A | b] is never materialised: acm_linear_system_qr reduces its rows on
+ * the GPU into the (k+1)x(k+1) upper-triangular R factor of a tall-skinny QR
+ * (r_factor: device, packed row-major upper triangle; error_flag: device int,
+ * set on the reference's NumericalError path).  acm_linear_estimation then
+ * solves R_A x = z on the host with nalgebra's SVD::solve(eps) semantics
+ * (eps = f64::EPSILON for KB, 1e-10 otherwise), applies the model's clamps
+ * and validation, and writes the estimate into cam->params (k = 4 KB,
+ * 3 RadTan, 1 DS/UCM/EUCM; FOV's grid search is not supported). */
+ACM_API int acm_linear_system_columns(int model);
+ACM_API size_t acm_linear_system_qr_workspace_size(int model, size_t n);
+ACM_API int acm_linear_system_qr(const acm_camera *cam, size_t n,
+                                 const double *points_3d, int layout,
+                                 const double *points_2d, double *r_factor,
+                                 int *error_flag, void *workspace,
+                                 size_t workspace_bytes, void *stream);
+ACM_API size_t acm_linear_estimation_workspace_size(int model, size_t n);
+ACM_API int acm_linear_estimation(acm_camera *cam, size_t n,
+                                  const double *points_3d, int layout,
+                                  const double *points_2d, void *workspace,
+                                  size_t workspace_bytes, void *stream);
+
+/* Bounded Levenberg-Marquardt over the fused normal equations: the
+ * apex-solver call of camera_converter.rs:381-420.  Each evaluation runs
+ * acm_normal_equations, then (if allreduce != NULL) hands the device result
+ * vector [JtJ | Jtr | cost | n_valid] to the callback for a cross-rank sum
+ * (e.g. RCCL all-reduce), copies it to the host and solves the damped
+ * P x P system by Cholesky.  cam->params: initial value in, optimum out. */
+typedef struct acm_lm_config {
+    int32_t max_iterations;      /* 100 (camera_converter.rs:411) */
+    int32_t invalid_policy;      /* ACM_INVALID_SKIP / _SENTINEL */
+    double cost_tolerance;       /* 1e-6 relative cost decrease */
+    double parameter_tolerance;  /* 1e-8 */
+    double gradient_tolerance;   /* 1e-6 on |Jtr|_inf */
+    double initial_damping;      /* mu0 (Marquardt-scaled), 1e-4 */
+    uint32_t has_bounds;
+    uint32_t reserved;
+    double lower[ACM_MAX_PARAMS]; /* set_variable_bounds */
+    double upper[ACM_MAX_PARAMS];
+} acm_lm_config;
+
+enum {
+    ACM_LM_MAX_ITERATIONS = 0,
+    ACM_LM_COST = 1,
+    ACM_LM_PARAMETER = 2,
+    ACM_LM_GRADIENT = 3,
+    ACM_LM_FAILED = 4
+};
+
+typedef struct acm_lm_summary {
+    int32_t iterations;
+    int32_t termination; /* ACM_LM_* */
+    int32_t evaluations;
+    int32_t reserved;
+    double initial_cost; /* 0.5 * sum ||r||^2 */
+    double final_cost;
+    double n_valid;
+} acm_lm_summary;
+
+typedef int (*acm_allreduce_fn)(void *ctx, double *device_buffer, size_t count,
+                                void *stream);
+
+ACM_API void acm_lm_default_config(acm_lm_config *cfg);
+ACM_API size_t acm_lm_workspace_size(int model, size_t n);
+ACM_API int acm_lm_optimize(acm_camera *cam, size_t n, const double *points_3d,
+                            int layout, const double *points_2d,
+                            const acm_lm_config *cfg, acm_allreduce_fn allreduce,
+                            void *allreduce_ctx, acm_lm_summary *summary,
+                            void *workspace, size_t workspace_bytes, void *stream);
+
 /* Exact median of the non-NaN values of `values` (the per-point errors of
  * acm_reprojection_stats), error_metrics.rs:103-111: the mean of ranks
  * m/2-1 and m/2 for even m, rank m/2 for odd m, m = n_valid (read from
@@ -202,6 +274,16 @@ ACM_API int acm_sample_points(const acm_camera *cam, size_t n_requested,
                               double *points_2d_out, double *points_3d_out,
                               uint64_t *counts, void *workspace,
                               size_t workspace_bytes, void *stream);
+/* Same over the cell range [cell_begin, cell_end) of the row-major grid (a
+ * multi-GPU shard: ranks take contiguous row ranges and concatenating their
+ * outputs in rank order reproduces the serial order).  counts[1] = cells in
+ * the range.  Workspace: acm_sample_points_workspace_size of the full grid
+ * is always enough. */
+ACM_API int acm_sample_points_range(const acm_camera *cam, size_t n_requested,
+                                    size_t cell_begin, size_t cell_end,
+                                    double *points_2d_out, double *points_3d_out,
+                                    uint64_t *counts, void *workspace,
+                                    size_t workspace_bytes, void *stream);
 
 /* Device-memory helpers so a host without HIP bindings (e.g. the Rust crate
  * through `extern "C"`) can own device buffers: thin wrappers over
