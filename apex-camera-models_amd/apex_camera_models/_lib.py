@@ -82,6 +82,7 @@ EXPORTED_SYMBOLS = (
     "acm_camera_init",
     "acm_validate_params",
     "acm_project",
+    "acm_project_f32",
     "acm_unproject",
     "acm_residual_jacobian",
     "acm_normal_equations_workspace_size",
@@ -102,6 +103,7 @@ EXPORTED_SYMBOLS = (
     "acm_sample_points_workspace_size",
     "acm_sample_points",
     "acm_sample_points_range",
+    "acm_undistort_image",
     "acm_set_device",
     "acm_device_malloc",
     "acm_device_free",
@@ -146,6 +148,8 @@ def load():
     L.acm_validate_params.restype = i
     L.acm_project.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp]
     L.acm_project.restype = i
+    L.acm_project_f32.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp]
+    L.acm_project_f32.restype = i
     L.acm_unproject.argtypes = [cam_p, sz, vp, vp, i, vp, vp]
     L.acm_unproject.restype = i
     L.acm_residual_jacobian.argtypes = [cam_p, sz, vp, i, vp, i, vp, vp, vp, vp]
@@ -189,6 +193,8 @@ def load():
     L.acm_median_workspace_size.restype = sz
     L.acm_median_valid.argtypes = [sz, vp, vp, ctypes.c_uint64, vp, vp, sz, vp]
     L.acm_median_valid.restype = i
+    L.acm_undistort_image.argtypes = [cam_p, ctypes.POINTER(ctypes.c_double), i, vp, vp, vp]
+    L.acm_undistort_image.restype = i
     L.acm_set_device.argtypes = [i]
     L.acm_set_device.restype = i
     L.acm_device_malloc.argtypes = [ctypes.POINTER(vp), sz]

@@ -210,26 +210,30 @@ class CameraModel:
         layout="soa", (3,N).  Returns (uv (N,2), status (N,) uint8, jac) where
         jac is (P,N,2) -- memory identical to a 2N x P column-major DMatrix --
         or None.  Failed points: uv = NaN, J = 0, status = error code.
+        A float32 input tensor selects the f32 kernels (acm_project_f32).
         """
         lay = _lib.LAYOUT_SOA if layout == "soa" else _lib.LAYOUT_AOS
+        pts = points_3d if isinstance(points_3d, torch.Tensor) else torch.as_tensor(
+            points_3d, dtype=torch.float64)
+        dt = torch.float32 if pts.dtype == torch.float32 else torch.float64
+        pts = pts.to("cuda", dt)
         if lay == _lib.LAYOUT_SOA:
-            pts = points_3d if isinstance(points_3d, torch.Tensor) else torch.as_tensor(points_3d)
-            pts = pts.to("cuda", torch.float64).reshape(3, -1).contiguous()
+            pts = pts.reshape(3, -1).contiguous()
             n = pts.shape[1]
         else:
-            pts = _as_device_f64(points_3d, 3)
+            pts = pts.reshape(-1, 3).contiguous()
             n = pts.shape[0]
         if out is not None:
             uv, st, jac = out
         else:
-            uv = torch.empty((n, 2), dtype=torch.float64, device=pts.device)
+            uv = torch.empty((n, 2), dtype=dt, device=pts.device)
             st = torch.empty((n,), dtype=torch.uint8, device=pts.device)
-            jac = (torch.empty((self.NUM_PARAMS, n, 2), dtype=torch.float64, device=pts.device)
+            jac = (torch.empty((self.NUM_PARAMS, n, 2), dtype=dt, device=pts.device)
                    if jacobian else None)
         cam = self.acm_camera()
-        _lib.check(_lib.load().acm_project(
-            ctypes.byref(cam), n, pts.data_ptr(), lay, uv.data_ptr(), st.data_ptr(),
-            jac.data_ptr() if jac is not None else None, _stream_handle()))
+        fn = _lib.load().acm_project_f32 if dt == torch.float32 else _lib.load().acm_project
+        _lib.check(fn(ctypes.byref(cam), n, pts.data_ptr(), lay, uv.data_ptr(), st.data_ptr(),
+                      jac.data_ptr() if jac is not None else None, _stream_handle()))
         return uv, st, jac
 
     def unproject_batch(self, points_2d, layout: str = "aos"):

@@ -100,3 +100,30 @@ def reprojection_median(errors: torch.Tensor, n_valid: int) -> float:
     _lib.check(L.acm_median_valid(errors.numel(), errors.data_ptr(), None, n_valid, out.data_ptr(),
                                   ws.data_ptr(), ws_bytes, _stream_handle()))
     return float(out.item())
+
+
+NEAREST, BILINEAR = 0, 1
+
+
+def undistort_image(input_image, camera_model: CameraModel, target_intrinsics=None,
+                    interpolation: int = BILINEAR):
+    """`undistort_image` (src/util/undistort.rs:14-49): input_image (H, W, 3)
+    uint8 (device or host), returns the (H, W, 3) uint8 device tensor."""
+    res = camera_model.get_resolution()
+    img = input_image if isinstance(input_image, torch.Tensor) else torch.as_tensor(input_image)
+    img = img.to("cuda", torch.uint8).contiguous()
+    if img.dim() != 3 or img.shape[2] != 3:
+        raise UtilError("expected an (H, W, 3) RGB8 image")
+    h, w = img.shape[0], img.shape[1]
+    if w != res.width or h != res.height:  # :23-28
+        raise UtilError(f"Image {w}x{h} doesn't match model {res.width}x{res.height}")
+    out = torch.empty_like(img)
+    cam = camera_model.acm_camera()
+    t = None
+    if target_intrinsics is not None:
+        ti = target_intrinsics
+        t = (ctypes.c_double * 4)(ti.fx, ti.fy, ti.cx, ti.cy)
+    _lib.check(_lib.load().acm_undistort_image(ctypes.byref(cam), t, interpolation,
+                                               img.data_ptr(), out.data_ptr(),
+                                               _stream_handle()))
+    return out

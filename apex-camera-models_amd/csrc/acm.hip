@@ -172,6 +172,45 @@ __global__ __launch_bounds__(kBlock) void k_project(acm_camera cam, size_t n,
     }
 }
 
+// ------------------------------------------------ project (+J), f32 sweep
+// The same model code evaluated in float (BASELINE config 5's f32 vs f64
+// tolerance sweep): float in / float out, 12 + 8 + 1 + 8P bytes per point.
+typedef float flt2 __attribute__((ext_vector_type(2)));
+
+template <class TagT, int LAYOUT, bool WJ, bool NT>
+__global__ __launch_bounds__(kBlock) void k_project_f32(acm_camera cam, size_t n,
+                                                        const float* __restrict__ pts,
+                                                        float* __restrict__ uv,
+                                                        uint8_t* __restrict__ status,
+                                                        float* __restrict__ jac) {
+    using M = typename TagT::template type<float>;
+    constexpr int P = M::P;
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const Cam<float> c = make_cam<float>(cam);
+    float x, y, z;
+    if (LAYOUT == ACM_LAYOUT_AOS) {
+        x = pts[3 * i]; y = pts[3 * i + 1]; z = pts[3 * i + 2];
+    } else {
+        x = pts[i]; y = pts[n + i]; z = pts[2 * n + i];
+    }
+    float u, v, ju[P], jv[P];
+    const uint8_t st = M::template project<WJ>(c, x, y, z, u, v, ju, jv);
+    const bool ok = st == ST_OK;
+    auto put = [&](float* p, float a, float b) {
+        flt2 val = {a, b};
+        if (NT) __builtin_nontemporal_store(val, reinterpret_cast<flt2*>(p));
+        else *reinterpret_cast<flt2*>(p) = val;
+    };
+    put(uv + 2 * i, ok ? u : __builtin_nanf(""), ok ? v : __builtin_nanf(""));
+    status[i] = st;
+    if (WJ) {
+        const size_t col = 2 * n;
+#pragma unroll
+        for (int p = 0; p < P; ++p) put(jac + p * col + 2 * i, ok ? ju[p] : 0.0f, ok ? jv[p] : 0.0f);
+    }
+}
+
 // --------------------------------------------------------------- unproject
 template <class TagT, int LAYOUT>
 __global__ __launch_bounds__(kBlock) void k_unproject(acm_camera cam, size_t n,
@@ -846,6 +885,74 @@ __global__ __launch_bounds__(kBlock) void k_tsqr_final(const double* __restrict_
     }
 }
 
+// ---------------------------------------------------------- undistort_image
+// undistort.rs:14-105: per output pixel, the ray ((u-cx')/fx', (v-cy')/fy', 1)
+// of the target intrinsics is projected through the camera model and the
+// input RGB8 image is sampled there (nearest or bilinear, the reference's
+// rounding/clamping); failed projections / out-of-image samples stay black.
+// 64 x 4 workgroups: a wave covers 64 consecutive output pixels of a row.
+__device__ __forceinline__ int rust_as_i32(double v) {
+    if (v != v) return 0;  // Rust `as` casts saturate and map NaN to 0
+    if (v >= 2147483647.0) return 2147483647;
+    if (v <= -2147483648.0) return (-2147483647 - 1);
+    return (int)v;
+}
+
+template <class TagT, bool BILINEAR>
+__global__ __launch_bounds__(kBlock) void k_undistort(acm_camera cam, double tfx, double tfy,
+                                                      double tcx, double tcy,
+                                                      const uint8_t* __restrict__ img,
+                                                      uint8_t* __restrict__ out) {
+    using M = typename TagT::template type<double>;
+    const uint32_t w = cam.width, h = cam.height;
+    const uint32_t u_out = blockIdx.x * 64 + (threadIdx.x & 63);
+    const uint32_t v_out = blockIdx.y * (kBlock / 64) + (threadIdx.x >> 6);
+    if (u_out >= w || v_out >= h) return;
+    const Cam<double> c = make_cam<double>(cam);
+    const double x_norm = ((double)u_out - tcx) / tfx;  // :35-36
+    const double y_norm = ((double)v_out - tcy) / tfy;
+    double su, sv;
+    const uint8_t st = M::template project<false>(c, x_norm, y_norm, 1.0, su, sv, nullptr, nullptr);
+    uint8_t r = 0, g = 0, b = 0;
+    if (st == ST_OK) {
+        if (!BILINEAR) {  // :61-69
+            const int u = rust_as_i32(round(su)), v = rust_as_i32(round(sv));
+            if (u >= 0 && u < (int)w && v >= 0 && v < (int)h) {
+                const uint8_t* p = img + ((size_t)v * w + (size_t)u) * 3;
+                r = p[0]; g = p[1]; b = p[2];
+            }
+        } else {  // :71-103
+            const double x0 = floor(su), y0 = floor(sv);
+            const double x1 = x0 + 1.0, y1 = y0 + 1.0;
+            if (!(x0 < 0.0 || x1 >= (double)w || y0 < 0.0 || y1 >= (double)h)) {
+                const uint32_t x0u = (uint32_t)x0, y0u = (uint32_t)y0;
+                const uint32_t x1u = (uint32_t)x1, y1u = (uint32_t)y1;
+                const uint8_t* p00 = img + ((size_t)y0u * w + x0u) * 3;
+                const uint8_t* p10 = img + ((size_t)y0u * w + x1u) * 3;
+                const uint8_t* p01 = img + ((size_t)y1u * w + x0u) * 3;
+                const uint8_t* p11 = img + ((size_t)y1u * w + x1u) * 3;
+                const double wx = su - x0, wy = sv - y0;
+                const double wx_inv = 1.0 - wx, wy_inv = 1.0 - wy;
+                uint8_t res[3];
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    const double val = (double)p00[ch] * wx_inv * wy_inv +
+                                       (double)p10[ch] * wx * wy_inv +
+                                       (double)p01[ch] * wx_inv * wy + (double)p11[ch] * wx * wy;
+                    double q = round(val);
+                    q = q < 0.0 ? 0.0 : (q > 255.0 ? 255.0 : q);
+                    res[ch] = (uint8_t)q;
+                }
+                r = res[0]; g = res[1]; b = res[2];
+            }
+        }
+    }
+    uint8_t* o = out + ((size_t)v_out * w + u_out) * 3;
+    o[0] = r;
+    o[1] = g;
+    o[2] = b;
+}
+
 static unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 static int check_cam(const acm_camera* cam) {
@@ -973,6 +1080,34 @@ ACM_API int acm_project(const acm_camera* cam, size_t n, const double* points_3d
             else by_var(SOA{}, std::false_type{});
         }
         return check_launch("acm_project");
+    });
+}
+
+ACM_API int acm_project_f32(const acm_camera* cam, size_t n, const float* points_3d, int layout,
+                            float* points_2d, uint8_t* status, float* jacobian, void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if ((rc = check_layout(layout))) return rc;
+    if (n == 0) return ACM_SUCCESS;
+    if (!points_3d || !points_2d || !status) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t out_bytes = n * (9 + (jacobian ? 8 * (size_t)acm_num_params(cam->model) : 0));
+    const bool nt = out_bytes > kNtThresholdBytes;
+    return dispatch_model(cam->model, [&](auto tag) -> int {
+        using TagT = decltype(tag);
+        const dim3 g(grid_for(n)), b(kBlock);
+#define ACM_F32(L, WJ, NT)                                                                     \
+    hipLaunchKernelGGL((k_project_f32<TagT, L, WJ, NT>), g, b, 0, s, *cam, n, points_3d,       \
+                       points_2d, status, jacobian)
+        if (layout == ACM_LAYOUT_AOS) {
+            if (jacobian) { if (nt) ACM_F32(ACM_LAYOUT_AOS, true, true); else ACM_F32(ACM_LAYOUT_AOS, true, false); }
+            else { if (nt) ACM_F32(ACM_LAYOUT_AOS, false, true); else ACM_F32(ACM_LAYOUT_AOS, false, false); }
+        } else {
+            if (jacobian) { if (nt) ACM_F32(ACM_LAYOUT_SOA, true, true); else ACM_F32(ACM_LAYOUT_SOA, true, false); }
+            else { if (nt) ACM_F32(ACM_LAYOUT_SOA, false, true); else ACM_F32(ACM_LAYOUT_SOA, false, false); }
+        }
+#undef ACM_F32
+        return check_launch("acm_project_f32");
     });
 }
 
@@ -1271,6 +1406,30 @@ ACM_API int acm_median_valid(size_t n, const double* values, const double* n_val
     return check_launch("acm_median_valid");
 }
 
+
+ACM_API int acm_undistort_image(const acm_camera* cam, const double* target_intrinsics,
+                                int interpolation, const uint8_t* image, uint8_t* output,
+                                void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if (!image || !output) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (interpolation != ACM_INTERP_NEAREST && interpolation != ACM_INTERP_BILINEAR)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "interpolation must be NEAREST or BILINEAR");
+    const double* t = target_intrinsics ? target_intrinsics : cam->params;  // :30
+    if (cam->width == 0 || cam->height == 0) return ACM_SUCCESS;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 g((cam->width + 63) / 64, (cam->height + kBlock / 64 - 1) / (kBlock / 64));
+    return dispatch_model(cam->model, [&](auto tag) -> int {
+        using TagT = decltype(tag);
+        if (interpolation == ACM_INTERP_BILINEAR)
+            hipLaunchKernelGGL((k_undistort<TagT, true>), g, dim3(kBlock), 0, s, *cam, t[0], t[1],
+                               t[2], t[3], image, output);
+        else
+            hipLaunchKernelGGL((k_undistort<TagT, false>), g, dim3(kBlock), 0, s, *cam, t[0],
+                               t[1], t[2], t[3], image, output);
+        return check_launch("acm_undistort_image");
+    });
+}
 
 static int hip_rc(hipError_t e, const char* what) {
     if (e == hipSuccess) return ACM_SUCCESS;

@@ -136,6 +136,13 @@ ACM_API int acm_project(const acm_camera *cam, size_t n,
                         const double *points_3d, int layout, double *points_2d,
                         uint8_t *status, double *jacobian, void *stream);
 
+/* The same projection evaluated in f32 (float buffers, same layouts; the
+ * camera parameters are rounded to float).  For the f32-vs-f64 tolerance
+ * sweep of BASELINE config 5; the reference itself is f64 only. */
+ACM_API int acm_project_f32(const acm_camera *cam, size_t n,
+                            const float *points_3d, int layout, float *points_2d,
+                            uint8_t *status, float *jacobian, void *stream);
+
 /* Batched CameraModel::unproject (mod.rs:271).  rays: 3N f64 out written in
  * `layout`; failed points: ray = NaN. */
 ACM_API int acm_unproject(const acm_camera *cam, size_t n,
@@ -284,6 +291,16 @@ ACM_API int acm_sample_points_range(const acm_camera *cam, size_t n_requested,
                                     double *points_2d_out, double *points_3d_out,
                                     uint64_t *counts, void *workspace,
                                     size_t workspace_bytes, void *stream);
+
+/* util::undistort_image (src/util/undistort.rs:14-105).  image/output:
+ * device RGB8 row-major, cam->width x cam->height (the reference requires
+ * the image to match the model resolution).  target_intrinsics: host
+ * [fx fy cx cy] or NULL for the camera's own (:30).  Pixels whose ray fails
+ * to project or whose sample falls outside the image are written 0. */
+enum { ACM_INTERP_NEAREST = 0, ACM_INTERP_BILINEAR = 1 };
+ACM_API int acm_undistort_image(const acm_camera *cam, const double *target_intrinsics,
+                                int interpolation, const uint8_t *image,
+                                uint8_t *output, void *stream);
 
 /* Device-memory helpers so a host without HIP bindings (e.g. the Rust crate
  * through `extern "C"`) can own device buffers: thin wrappers over

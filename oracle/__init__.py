@@ -65,6 +65,9 @@ def lib():
         L.oracle_sample_points.restype = sz
         L.oracle_linear_estimation_system.argtypes = [ctypes.c_int, dp, sz, dp, dp, dp, dp]
         L.oracle_linear_estimation_system.restype = ctypes.c_int
+        L.oracle_undistort_image.argtypes = [ctypes.c_int, dp, u32, u32, dp, ctypes.c_int,
+                                             u8p, u8p]
+        L.oracle_undistort_image.restype = None
         _lib = L
     return _lib
 
@@ -179,3 +182,14 @@ def linear_estimation_system(model, params, xyz, uv):
     if k < 0:
         return None, None, k
     return A.reshape(-1)[: 2 * n * k].reshape(2 * n, k).copy(), b, k
+
+
+def undistort_image(model, params, w, h, target, bilinear, img):
+    """img: (h, w, 3) uint8 -> (h, w, 3) uint8 (src/util/undistort.rs:14-49)."""
+    params = _f64(params)
+    target = _f64(target)
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    out = np.empty_like(img)
+    lib().oracle_undistort_image(model, _dp(params), w, h, _dp(target), int(bilinear),
+                                 _u8p(img), _u8p(out))
+    return out

@@ -766,3 +766,68 @@ int oracle_linear_estimation_system(int model, const double *params, size_t n,
     }
     return -1;
 }
+
+/* ---------------------------------------------------------------- undistort */
+/* Rust `f64 as i32`: saturating, NaN -> 0 */
+static int rust_as_i32(double v) {
+    if (v != v) return 0;
+    if (v >= 2147483647.0) return 2147483647;
+    if (v <= -2147483648.0) return (-2147483647 - 1);
+    return (int)v;
+}
+
+/* src/util/undistort.rs:51-105 (interpolate_pixel).  Returns 1 and writes
+ * rgb if the sample exists. */
+static int interpolate_pixel(const uint8_t *img, uint32_t w, uint32_t h, double x,
+                             double y, int bilinear, uint8_t rgb[3]) {
+    if (!bilinear) {                                             /* :61-69 */
+        int u = rust_as_i32(round(x)), v = rust_as_i32(round(y));
+        if (u >= 0 && u < (int)w && v >= 0 && v < (int)h) {
+            const uint8_t *p = img + ((size_t)v * w + (size_t)u) * 3;
+            rgb[0] = p[0]; rgb[1] = p[1]; rgb[2] = p[2];
+            return 1;
+        }
+        return 0;
+    }
+    double x0 = floor(x), y0 = floor(y);                         /* :71-74 */
+    double x1 = x0 + 1.0, y1 = y0 + 1.0;
+    if (x0 < 0.0 || x1 >= (double)w || y0 < 0.0 || y1 >= (double)h) return 0;
+    uint32_t x0u = (uint32_t)x0, y0u = (uint32_t)y0, x1u = (uint32_t)x1, y1u = (uint32_t)y1;
+    const uint8_t *p00 = img + ((size_t)y0u * w + x0u) * 3;
+    const uint8_t *p10 = img + ((size_t)y0u * w + x1u) * 3;
+    const uint8_t *p01 = img + ((size_t)y1u * w + x0u) * 3;
+    const uint8_t *p11 = img + ((size_t)y1u * w + x1u) * 3;
+    double wx = x - x0, wy = y - y0;                             /* :89-92 */
+    double wx_inv = 1.0 - wx, wy_inv = 1.0 - wy;
+    for (int c = 0; c < 3; ++c) {                                /* :95-101 */
+        double val = (double)p00[c] * wx_inv * wy_inv + (double)p10[c] * wx * wy_inv +
+                     (double)p01[c] * wx_inv * wy + (double)p11[c] * wx * wy;
+        double r = round(val);
+        r = r < 0.0 ? 0.0 : (r > 255.0 ? 255.0 : r);
+        rgb[c] = (uint8_t)r;
+    }
+    return 1;
+}
+
+/* src/util/undistort.rs:14-49 (undistort_image).  img/out: row-major RGB8,
+ * w x h = the model's resolution; target: fx fy cx cy. */
+void oracle_undistort_image(int model, const double *params, uint32_t w, uint32_t h,
+                            const double *target, int bilinear, const uint8_t *img,
+                            uint8_t *out) {
+    memset(out, 0, (size_t)w * h * 3);                           /* :31 */
+    for (uint32_t v_out = 0; v_out < h; ++v_out) {
+        for (uint32_t u_out = 0; u_out < w; ++u_out) {
+            double x_norm = ((double)u_out - target[2]) / target[0]; /* :35 */
+            double y_norm = ((double)v_out - target[3]) / target[1];
+            double ray[3] = {x_norm, y_norm, 1.0};
+            double uv[2];
+            if (oracle_project(model, params, w, h, ray, uv) == OR_OK) {
+                uint8_t rgb[3];
+                if (interpolate_pixel(img, w, h, uv[0], uv[1], bilinear, rgb)) {
+                    uint8_t *o = out + ((size_t)v_out * w + u_out) * 3;
+                    o[0] = rgb[0]; o[1] = rgb[1]; o[2] = rgb[2];
+                }
+            }
+        }
+    }
+}

@@ -112,6 +112,12 @@ int oracle_linear_estimation_system(int model, const double *params,
                                     size_t n, const double *xyz,
                                     const double *uv, double *A, double *b);
 
+/* undistort_image (src/util/undistort.rs:14-105): RGB8 row-major w x h,
+ * target = [fx fy cx cy], bilinear 0 = Nearest, 1 = Bilinear. */
+void oracle_undistort_image(int model, const double *params, uint32_t w,
+                            uint32_t h, const double *target, int bilinear,
+                            const uint8_t *img, uint8_t *out);
+
 #ifdef __cplusplus
 }
 #endif

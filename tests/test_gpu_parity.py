@@ -245,3 +245,25 @@ def test_empty_batch_is_noop():
     m = _model_obj(2, params, w, h)
     uv, st, J = m.project_batch(torch.empty((0, 3), dtype=torch.float64), jacobian=True)
     assert uv.shape == (0, 2) and st.shape == (0,) and J.shape == (8, 0, 2)
+
+
+@pytest.mark.parametrize("model", range(7))
+def test_f32_path_tracks_f64(golden_dir, model):
+    """f32 evaluation of the same model code (config 5 sweep): masks may only
+    differ where an f64 threshold test is within f32 rounding; values within
+    f32 accuracy of the f64 oracle."""
+    import torch
+    g, params, w, h = _golden(golden_dir, model)
+    keep = _finite_rows(g) & (np.abs(g["xyz"]) < 1e3).all(1)
+    xyz = g["xyz"][keep]
+    m = _model_obj(model, params, w, h)
+    uv, st, J = m.project_batch(torch.as_tensor(xyz, dtype=torch.float32), jacobian=True)
+    assert uv.dtype == torch.float32 and J.dtype == torch.float32
+    st = st.cpu().numpy()
+    st0 = g["proj_status"][keep]
+    agree = (st == st0).mean()
+    assert agree > 0.99, agree
+    both = (st == 0) & (st0 == 0)
+    u0 = g["uv"][keep][both]
+    err = np.abs(uv.cpu().numpy()[both].astype(np.float64) - u0) / np.maximum(np.abs(u0), 1.0)
+    assert np.nanmax(err) < 1e-4

@@ -1,0 +1,203 @@
+"""Secondary measurements for BASELINE.json configs 1, 3, 4 and 5 (config 2 is
+bench.py, the headline).  One JSON line per measurement; not the driver's
+bench contract.
+
+  python tools/bench_configs.py [--configs 1,3,4,5] [--scale 1.0]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "apex-camera-models_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def emit(d):
+    print(json.dumps(d), flush=True)
+
+
+def timed(fn, reps=10, warm=2):
+    import torch
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    t = sorted(a.elapsed_time(b) for a, b in ev)
+    return t[len(t) // 2]
+
+
+def config1():
+    """Pinhole project/unproject, 1k points, CPU reference path (oracle)
+    500/500/320/240 @ 640x480 (tests/projection_accuracy.rs:50-53)."""
+    import oracle as O
+    p = [500.0, 500.0, 320.0, 240.0]
+    rng = np.random.default_rng(1)
+    pts = np.stack([rng.uniform(-0.3, 0.3, 1000), rng.uniform(-0.2, 0.2, 1000),
+                    rng.uniform(0.5, 4.0, 1000)], 1)
+    t0 = time.perf_counter()
+    for _ in range(100):
+        uv, st, _ = O.project(0, p, 640, 480, pts)
+        ray, st2 = O.unproject(0, p, 640, 480, uv[st == 0])
+    dt = (time.perf_counter() - t0) / 100
+    pn = pts[st == 0] / np.linalg.norm(pts[st == 0], axis=1, keepdims=True)
+    dots = (pn * ray).sum(1)
+    emit({"config": 1, "what": "pinhole project+unproject 1k pts, CPU oracle (1 thread)",
+          "ms": round(dt * 1e3, 4), "Mpoints_per_s": round(1000 / dt / 1e6, 2),
+          "valid": int((st == 0).sum()), "min_round_trip_dot": float(dots.min())})
+
+
+def config3(n_target):
+    """DS residual+J and fused normal equations over ~10M KB-sampled
+    correspondences, inside the bounded LM of camera_converter.rs:355-488."""
+    import torch
+    from apex_camera_models import KannalaBrandtModel, Resolution, _lib, conversion, factors
+    from apex_camera_models import samples, util
+    kp, (w, h) = samples.SAMPLES[2]
+    src = KannalaBrandtModel._from_params(kp, Resolution(w, h))
+    t0 = time.perf_counter()
+    uv, xyz = util.sample_points(src, n_target)
+    torch.cuda.synchronize()
+    t_sample = time.perf_counter() - t0
+    n = xyz.shape[0]
+    model = conversion._init_target("double_sphere", src)
+    model.linear_estimation(xyz, uv)
+    f = factors.DoubleSphereCameraParamsFactor(xyz, uv, Resolution(w, h))
+    p = model.params()
+    res = torch.empty((n, 2), dtype=torch.float64, device="cuda")
+    jac = torch.empty((6, n, 2), dtype=torch.float64, device="cuda")
+    cam = model.acm_camera()
+    L = _lib.load()
+    sh = torch.cuda.current_stream().cuda_stream
+
+    def rj():
+        L.acm_residual_jacobian(ctypes.byref(cam), n, xyz.data_ptr(), 0, uv.data_ptr(), 0,
+                                res.data_ptr(), jac.data_ptr(), None, sh)
+
+    ms_rj = timed(rj)
+    out = torch.empty((6 * 6 + 6 + 2,), dtype=torch.float64, device="cuda")
+    ms_ne = timed(lambda: f.normal_equations(p, out))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    met = conversion.convert(src, "double_sphere", xyz, uv)
+    t_conv = time.perf_counter() - t0
+    emit({"config": 3, "what": "DS residual+J (2N x 6) kernel", "points": n,
+          "ms": round(ms_rj, 4), "Mpoints_per_s": round(n / ms_rj / 1e3, 1),
+          "GBps": round(153 * n / ms_rj / 1e6, 1)})
+    emit({"config": 3, "what": "DS fused normal equations (JtJ, Jtr, cost)", "points": n,
+          "ms": round(ms_ne, 4), "Mpoints_per_s": round(n / ms_ne / 1e3, 1),
+          "GBps": round(40 * n / ms_ne / 1e6, 1)})
+    emit({"config": 3, "what": "KB->DS conversion: linear estimation + bounded LM (wall)",
+          "points": n, "sample_points_s": round(t_sample, 4), "convert_s": round(t_conv, 4),
+          "lm_iterations": met.lm_iterations, "termination": met.lm_termination,
+          "final_mean_px": met.final_reprojection_error.mean,
+          "initial_mean_px": met.initial_reprojection_error.mean})
+
+
+def config4(n_per_model):
+    """Every model: project -> unproject round trip (two launches, uv
+    intermediate in HBM), plus the round-trip error sum (RCCL all-reduce on
+    >1 rank)."""
+    import torch
+    from apex_camera_models import _lib, samples
+    from apex_camera_models.camera import MODEL_CLASSES, Resolution
+    names = {0: "pinhole", 1: "rad_tan", 2: "kannala_brandt", 3: "double_sphere", 4: "ucm",
+             5: "eucm"}
+    pts = samples.synthetic_points_device(n_per_model)
+    L = _lib.load()
+    for mid, name in names.items():
+        params, (w, h) = samples.SAMPLES[mid]
+        m = MODEL_CLASSES[name]._from_params(params, Resolution(w, h))
+        cam = m.acm_camera()
+        uv = torch.empty((n_per_model, 2), dtype=torch.float64, device="cuda")
+        st = torch.empty((n_per_model,), dtype=torch.uint8, device="cuda")
+        ray = torch.empty((n_per_model, 3), dtype=torch.float64, device="cuda")
+        st2 = torch.empty((n_per_model,), dtype=torch.uint8, device="cuda")
+        sh = torch.cuda.current_stream().cuda_stream
+
+        def rt():
+            L.acm_project(ctypes.byref(cam), n_per_model, pts.data_ptr(), 0, uv.data_ptr(),
+                          st.data_ptr(), None, sh)
+            L.acm_unproject(ctypes.byref(cam), n_per_model, uv.data_ptr(), ray.data_ptr(), 0,
+                            st2.data_ptr(), sh)
+
+        ms = timed(rt)
+        ms_u = timed(lambda: L.acm_unproject(ctypes.byref(cam), n_per_model, uv.data_ptr(),
+                                             ray.data_ptr(), 0, st2.data_ptr(), sh))
+        ok = (st == 0) & (st2 == 0) & torch.isfinite(pts).all(1)
+        pn = pts[ok] / torch.linalg.norm(pts[ok], dim=1, keepdim=True)
+        err = torch.linalg.norm(ray[ok] - pn, dim=1)
+        emit({"config": 4, "model": name, "points": n_per_model,
+              "round_trip_ms": round(ms, 4), "round_trip_Mpoints_per_s": round(
+                  n_per_model / ms / 1e3, 1),
+              "round_trip_GBps": round(82 * n_per_model / ms / 1e6, 1),
+              "unproject_ms": round(ms_u, 4),
+              "unproject_GBps": round(41 * n_per_model / ms_u / 1e6, 1),
+              "round_trip_ok": int(ok.sum()), "max_round_trip_err": float(err.max()),
+              "sum_sq_err": float((err * err).sum())})
+        del uv, st, ray, st2
+    torch.cuda.empty_cache()
+
+
+def config5(n_cells):
+    """KB -> DS on ~1e8 sampled correspondences (10000 x 10000 grid) + the
+    f32-vs-f64 sweep of the DS projection at the optimum."""
+    import torch
+    from apex_camera_models import KannalaBrandtModel, Resolution, conversion, samples, util
+    kp, (w, h) = samples.SAMPLES[2]
+    src = KannalaBrandtModel._from_params(kp, Resolution(w, h))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    uv, xyz = util.sample_points(src, n_cells)
+    torch.cuda.synchronize()
+    t_s = time.perf_counter() - t0
+    n = xyz.shape[0]
+    t0 = time.perf_counter()
+    met = conversion.convert(src, "double_sphere", xyz, uv)
+    t_c = time.perf_counter() - t0
+    emit({"config": 5, "what": "KB->DS conversion (sample_points + linear_estimation + LM)",
+          "requested": n_cells, "correspondences": n, "sample_points_s": round(t_s, 4),
+          "convert_s": round(t_c, 4), "lm_iterations": met.lm_iterations,
+          "termination": met.lm_termination,
+          "final_mean_px": met.final_reprojection_error.mean,
+          "final_rmse_px": met.final_reprojection_error.rmse})
+    ds = met.model
+    uv64, st64, _ = ds.project_batch(xyz)
+    uv32, st32, _ = ds.project_batch(xyz.to(torch.float32))
+    both = (st64 == 0) & (st32 == 0)
+    rel = ((uv32[both].double() - uv64[both]).abs() /
+           uv64[both].abs().clamp(min=1.0)).max()
+    emit({"config": 5, "what": "f32 vs f64 DS projection sweep at the optimum",
+          "points": n, "mask_disagreements": int((st64 != st32).sum()),
+          "max_rel_err_f32": float(rel)})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="1,3,4,5")
+    ap.add_argument("--scale", type=float, default=1.0)
+    a = ap.parse_args()
+    cs = a.configs.split(",")
+    if "1" in cs:
+        config1()
+    if "3" in cs:
+        config3(int(10_000_000 * a.scale))
+    if "4" in cs:
+        config4(int(6_250_000 * a.scale))
+    if "5" in cs:
+        config5(int(100_000_000 * a.scale))
+
+
+if __name__ == "__main__":
+    main()
