@@ -120,6 +120,10 @@ __device__ __forceinline__ void st1(uint8_t* p, uint8_t v) {
 // (profiles/r01_sweep_project.log).
 enum { kVarNT = 1, kVarGrid = 2, kVarTwo = 4 };
 static int g_project_variant = -1;
+// Residual+J: plain stores by default.  Unlike project+J, non-temporal stores
+// measured slower here (DS, 9.3M points: 0.273 ms plain vs 0.310 ms nt,
+// profiles/r01_configs.log); -1 = auto (nt above kNtThresholdBytes), 1 = on.
+static int g_residual_nt = 0;
 constexpr size_t kNtThresholdBytes = 256ull << 20;
 
 template <class TagT, int LAYOUT, bool WJ, bool NT>
@@ -212,7 +216,13 @@ __global__ __launch_bounds__(kBlock) void k_project_f32(acm_camera cam, size_t n
 }
 
 // --------------------------------------------------------------- unproject
-template <class TagT, int LAYOUT>
+template <bool NT>
+__device__ __forceinline__ void st1d(double* p, double v) {
+    if (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <class TagT, int LAYOUT, bool NT>
 __global__ __launch_bounds__(kBlock) void k_unproject(acm_camera cam, size_t n,
                                                       const double* __restrict__ uv,
                                                       double* __restrict__ rays,
@@ -226,19 +236,19 @@ __global__ __launch_bounds__(kBlock) void k_unproject(acm_camera cam, size_t n,
     const uint8_t st = M::unproject(c, q.x, q.y, X, Y, Z);
     if (st != ST_OK) X = Y = Z = __builtin_nan("");
     if (LAYOUT == ACM_LAYOUT_AOS) {
-        rays[3 * i] = X;
-        rays[3 * i + 1] = Y;
-        rays[3 * i + 2] = Z;
+        st1d<NT>(rays + 3 * i, X);
+        st1d<NT>(rays + 3 * i + 1, Y);
+        st1d<NT>(rays + 3 * i + 2, Z);
     } else {
-        rays[i] = X;
-        rays[n + i] = Y;
-        rays[2 * n + i] = Z;
+        st1d<NT>(rays + i, X);
+        st1d<NT>(rays + n + i, Y);
+        st1d<NT>(rays + 2 * n + i, Z);
     }
-    status[i] = st;
+    st1<NT>(status + i, st);
 }
 
 // -------------------------------------------------- residual + Jacobian
-template <class TagT, int LAYOUT, bool WJ>
+template <class TagT, int LAYOUT, bool WJ, bool NT>
 __global__ __launch_bounds__(kBlock) void k_residual(acm_camera cam, size_t n,
                                                      const double* __restrict__ pts,
                                                      const double* __restrict__ obs,
@@ -257,15 +267,12 @@ __global__ __launch_bounds__(kBlock) void k_residual(acm_camera cam, size_t n,
     const uint8_t st = M::template project<WJ>(c, x, y, z, u, v, ju, jv);
     const bool ok = st == ST_OK;
     const double sent = policy == ACM_INVALID_SENTINEL ? 1e6 : 0.0;
-    *reinterpret_cast<double2*>(res + 2 * i) =
-        ok ? make_double2(u - o.x, v - o.y) : make_double2(sent, sent);
-    if (status) status[i] = st;
+    st2<NT>(res + 2 * i, ok ? u - o.x : sent, ok ? v - o.y : sent);
+    if (status) st1<NT>(status + i, st);
     if (WJ) {
         const size_t col = 2 * n;
 #pragma unroll
-        for (int p = 0; p < P; ++p)
-            *reinterpret_cast<double2*>(jac + p * col + 2 * i) =
-                ok ? make_double2(ju[p], jv[p]) : make_double2(0.0, 0.0);
+        for (int p = 0; p < P; ++p) st2<NT>(jac + p * col + 2 * i, ok ? ju[p] : 0.0, ok ? jv[p] : 0.0);
     }
 }
 
@@ -955,6 +962,15 @@ __global__ __launch_bounds__(kBlock) void k_undistort(acm_camera cam, double tfx
 
 static unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// Host-side per-camera constants folded into unused parameter slots before a
+// launch.  FOV: params[8] = tan(w / 2) (fov.rs:297, :340), evaluated once by
+// the host libm (the same glibc tan the reference's f64::tan calls) instead
+// of once per lane by OCML.
+static acm_camera prep(acm_camera c) {
+    if (c.model == ACM_FOV) c.params[8] = std::tan(c.params[4] / 2.0);
+    return c;
+}
+
 static int check_cam(const acm_camera* cam) {
     if (!cam) return fail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
     const int p = acm_num_params(cam->model);
@@ -1058,7 +1074,7 @@ ACM_API int acm_project(const acm_camera* cam, size_t n, const double* points_3d
                                             : grid_for(n);
             if ((V & kVarGrid) && blocks > 256u * 8u) blocks = 256u * 8u;
             hipLaunchKernelGGL((k_project<TagT, L, WJ, V>), dim3(blocks), dim3(kBlock), 0, s,
-                               *cam, n, points_3d, points_2d, status, jacobian);
+                               prep(*cam), n, points_3d, points_2d, status, jacobian);
         };
         auto by_var = [&](auto lay_c, auto wj_c) {
             switch (var) {
@@ -1097,7 +1113,7 @@ ACM_API int acm_project_f32(const acm_camera* cam, size_t n, const float* points
         using TagT = decltype(tag);
         const dim3 g(grid_for(n)), b(kBlock);
 #define ACM_F32(L, WJ, NT)                                                                     \
-    hipLaunchKernelGGL((k_project_f32<TagT, L, WJ, NT>), g, b, 0, s, *cam, n, points_3d,       \
+    hipLaunchKernelGGL((k_project_f32<TagT, L, WJ, NT>), g, b, 0, s, prep(*cam), n, points_3d,       \
                        points_2d, status, jacobian)
         if (layout == ACM_LAYOUT_AOS) {
             if (jacobian) { if (nt) ACM_F32(ACM_LAYOUT_AOS, true, true); else ACM_F32(ACM_LAYOUT_AOS, true, false); }
@@ -1122,12 +1138,12 @@ ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
         const dim3 g(grid_for(n)), b(kBlock);
-        if (layout == ACM_LAYOUT_AOS)
-            hipLaunchKernelGGL((k_unproject<TagT, ACM_LAYOUT_AOS>), g, b, 0, s, *cam, n, points_2d,
-                               rays, status);
-        else
-            hipLaunchKernelGGL((k_unproject<TagT, ACM_LAYOUT_SOA>), g, b, 0, s, *cam, n, points_2d,
-                               rays, status);
+        const bool nt = n * 25 > kNtThresholdBytes;  // rays + status written once
+#define ACM_UNP(L, NT) \
+    hipLaunchKernelGGL((k_unproject<TagT, L, NT>), g, b, 0, s, prep(*cam), n, points_2d, rays, status)
+        if (layout == ACM_LAYOUT_AOS) { if (nt) ACM_UNP(ACM_LAYOUT_AOS, true); else ACM_UNP(ACM_LAYOUT_AOS, false); }
+        else { if (nt) ACM_UNP(ACM_LAYOUT_SOA, true); else ACM_UNP(ACM_LAYOUT_SOA, false); }
+#undef ACM_UNP
         return check_launch("acm_unproject");
     });
 }
@@ -1148,9 +1164,19 @@ ACM_API int acm_residual_jacobian(const acm_camera* cam, size_t n, const double*
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
         const dim3 g(grid_for(n)), b(kBlock);
+        const size_t out_bytes =
+            n * (17 + (jacobian ? 16 * (size_t)acm_num_params(cam->model) : 0));
+        const bool nt = g_residual_nt < 0 ? out_bytes > kNtThresholdBytes : g_residual_nt == 1;
 #define ACM_LAUNCH_RES(L, WJ)                                                                   \
-    hipLaunchKernelGGL((k_residual<TagT, L, WJ>), g, b, 0, s, *cam, n, points_3d, points_2d_obs, \
-                       invalid_policy, residual, jacobian, status)
+    do {                                                                                        \
+        if (nt)                                                                                 \
+            hipLaunchKernelGGL((k_residual<TagT, L, WJ, true>), g, b, 0, s, prep(*cam), n, points_3d, \
+                               points_2d_obs, invalid_policy, residual, jacobian, status);      \
+        else                                                                                    \
+            hipLaunchKernelGGL((k_residual<TagT, L, WJ, false>), g, b, 0, s, prep(*cam), n,           \
+                               points_3d, points_2d_obs, invalid_policy, residual, jacobian,    \
+                               status);                                                         \
+    } while (0)
         if (layout == ACM_LAYOUT_AOS) {
             if (jacobian) ACM_LAUNCH_RES(ACM_LAYOUT_AOS, true);
             else ACM_LAUNCH_RES(ACM_LAYOUT_AOS, false);
@@ -1194,10 +1220,10 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
         double* sums = parts + (size_t)nb * K;
         if (layout == ACM_LAYOUT_AOS)
             hipLaunchKernelGGL((k_normal_eq<TagT, ACM_LAYOUT_AOS>), dim3(nb), dim3(kBlock), 0, s,
-                               *cam, n, points_3d, points_2d_obs, invalid_policy, parts);
+                               prep(*cam), n, points_3d, points_2d_obs, invalid_policy, parts);
         else
             hipLaunchKernelGGL((k_normal_eq<TagT, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s,
-                               *cam, n, points_3d, points_2d_obs, invalid_policy, parts);
+                               prep(*cam), n, points_3d, points_2d_obs, invalid_policy, parts);
         hipLaunchKernelGGL(k_sum_columns, dim3(K), dim3(kBlock), 0, s, parts, nb, K, sums);
         hipLaunchKernelGGL(k_ne_expand, dim3(1), dim3(64), 0, s, sums, P, result);
         return check_launch("acm_normal_equations");
@@ -1233,10 +1259,10 @@ ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double
         using TagT = decltype(tag);
         if (layout == ACM_LAYOUT_AOS)
             hipLaunchKernelGGL((k_reproj_pass1<TagT, ACM_LAYOUT_AOS>), dim3(nb), dim3(kBlock), 0, s,
-                               *cam, n, points_3d, points_2d, errs, p1);
+                               prep(*cam), n, points_3d, points_2d, errs, p1);
         else
             hipLaunchKernelGGL((k_reproj_pass1<TagT, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s,
-                               *cam, n, points_3d, points_2d, errs, p1);
+                               prep(*cam), n, points_3d, points_2d, errs, p1);
         hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb, tot);
         hipLaunchKernelGGL(k_reproj_pass2, dim3(nb), dim3(kBlock), 0, s, n, errs, tot, p2);
         hipLaunchKernelGGL(k_sum_columns, dim3(1), dim3(kBlock), 0, s, p2, nb, 1, var);
@@ -1295,11 +1321,11 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
     hipStream_t s = (hipStream_t)stream;
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
-        hipLaunchKernelGGL((k_sample_count<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, *cam,
+        hipLaunchKernelGGL((k_sample_count<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, prep(*cam),
                            g, cells, cnt);
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, cnt, nb, off, counts,
                            (uint64_t)cells);
-        hipLaunchKernelGGL((k_sample_write<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, *cam,
+        hipLaunchKernelGGL((k_sample_write<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, prep(*cam),
                            g, cells, off, points_2d_out, points_3d_out);
         return check_launch("acm_sample_points");
     });
@@ -1358,10 +1384,10 @@ ACM_API int acm_linear_system_qr(const acm_camera* cam, size_t n, const double* 
         constexpr int MOD = decltype(model_c)::value;
         constexpr int M = LinRows<MOD>::K + 1;
         if (layout == ACM_LAYOUT_AOS)
-            hipLaunchKernelGGL((k_tsqr<MOD, ACM_LAYOUT_AOS>), dim3(nb), dim3(kBlock), 0, s, *cam,
+            hipLaunchKernelGGL((k_tsqr<MOD, ACM_LAYOUT_AOS>), dim3(nb), dim3(kBlock), 0, s, prep(*cam),
                                n, points_3d, points_2d, parts, error_flag);
         else
-            hipLaunchKernelGGL((k_tsqr<MOD, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s, *cam,
+            hipLaunchKernelGGL((k_tsqr<MOD, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s, prep(*cam),
                                n, points_3d, points_2d, parts, error_flag);
         hipLaunchKernelGGL((k_tsqr_final<M>), dim3(1), dim3(kBlock), 0, s, parts, nb, r_factor);
     };
@@ -1422,10 +1448,10 @@ ACM_API int acm_undistort_image(const acm_camera* cam, const double* target_intr
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
         if (interpolation == ACM_INTERP_BILINEAR)
-            hipLaunchKernelGGL((k_undistort<TagT, true>), g, dim3(kBlock), 0, s, *cam, t[0], t[1],
+            hipLaunchKernelGGL((k_undistort<TagT, true>), g, dim3(kBlock), 0, s, prep(*cam), t[0], t[1],
                                t[2], t[3], image, output);
         else
-            hipLaunchKernelGGL((k_undistort<TagT, false>), g, dim3(kBlock), 0, s, *cam, t[0],
+            hipLaunchKernelGGL((k_undistort<TagT, false>), g, dim3(kBlock), 0, s, prep(*cam), t[0],
                                t[1], t[2], t[3], image, output);
         return check_launch("acm_undistort_image");
     });
@@ -1466,6 +1492,12 @@ ACM_API int acm_set_tuning(int key, int value) {
             return fail(ACM_ERR_INVALID_ARGUMENT, "variant must be -1 (auto) or 0..5");
         const int old = g_project_variant;
         g_project_variant = value;
+        return old;
+    }
+    if (key == ACM_TUNE_RESIDUAL_NT) {
+        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
+        const int old = g_residual_nt;
+        g_residual_nt = value;
         return old;
     }
     return fail(ACM_ERR_INVALID_ARGUMENT, "unknown tuning key");

@@ -249,7 +249,8 @@ struct KannalaBrandt {
         const bool small = fabs(ru) < T(kEps);
         T xc = small ? T(0) : mx / ru;
         T yc = small ? T(0) : my / ru;
-        T s = sin(theta), co = cos(theta);
+        T s, co;
+        sincos(theta, &s, &co);  // one OCML range reduction for both
         T px = s * xc, py = s * yc;
         T n = sqrt(px * px + py * py + co * co);
         X = px / n;
@@ -431,7 +432,7 @@ struct Fov {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], wf = c.p[4];
         T r2 = x * x + y * y;
         T r = sqrt(r2);
-        T tan_w_half = tan(wf / T(2));  // camera constant
+        const T tan_w_half = c.p[8];  // tan(w / 2), host-precomputed (acm.hip prep)
         T atan_wrd = atan2(T(2) * tan_w_half * r, z);
         const bool axis = r2 < T(kEpsSqrt);
         T rd = axis ? T(2) * tan_w_half / wf : atan_wrd / (r * wf);
@@ -456,14 +457,15 @@ struct Fov {
     __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
                                                         T& Z) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], wf = c.p[4];
-        T tan_w_2 = tan(wf / T(2));
+        const T tan_w_2 = c.p[8];  // tan(w / 2), host-precomputed
         T mul2 = tan_w_2 * T(2);
         T mx = (u - cx) / fx;
         T my = (v - cy) / fy;
         T rd = sqrt(mx * mx + my * my);
         T px = mx, py = my;
         if (mul2 > T(kEpsSqrt) && rd > T(kEpsSqrt)) {
-            T srw = sin(rd * wf), crw = cos(rd * wf);
+            T srw, crw;
+            sincos(rd * wf, &srw, &crw);
             T ru = srw / (rd * mul2);
             px = mx * ru / crw;
             py = my * ru / crw;

@@ -195,11 +195,12 @@ def main():
                          "traffic": traffic, "algorithmic_bytes_per_launch": bpp * n,
                          "kernel_ms": round(kern_ms, 5)},
         }
-        if not a.no_cpu_baseline:
+        if not a.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(model_id, params, w, h, n,
                                                a.cpu_baseline_seconds)
         print(json.dumps(res), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

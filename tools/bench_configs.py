@@ -85,6 +85,13 @@ def config3(n_target):
         L.acm_residual_jacobian(ctypes.byref(cam), n, xyz.data_ptr(), 0, uv.data_ptr(), 0,
                                 res.data_ptr(), jac.data_ptr(), None, sh)
 
+    old = L.acm_set_tuning(1, 0)
+    ms_rj_plain = timed(rj)
+    L.acm_set_tuning(1, 1)
+    ms_rj_nt = timed(rj)
+    L.acm_set_tuning(1, old)
+    emit({"config": 3, "what": "residual+J store policy A/B", "plain_ms": round(ms_rj_plain, 4),
+          "nt_ms": round(ms_rj_nt, 4)})
     ms_rj = timed(rj)
     out = torch.empty((6 * 6 + 6 + 2,), dtype=torch.float64, device="cuda")
     ms_ne = timed(lambda: f.normal_equations(p, out))
@@ -176,11 +183,15 @@ def config5(n_cells):
     uv64, st64, _ = ds.project_batch(xyz)
     uv32, st32, _ = ds.project_batch(xyz.to(torch.float32))
     both = (st64 == 0) & (st32 == 0)
-    rel = ((uv32[both].double() - uv64[both]).abs() /
-           uv64[both].abs().clamp(min=1.0)).max()
+    d = ((uv32.double() - uv64).abs() / uv64.abs().clamp(min=1.0)).max(dim=1).values
+    d = torch.where(both, d, torch.zeros_like(d))
+    i = int(d.argmax())
+    q = torch.quantile(d[both][:: max(1, int(both.sum()) // 1_000_000)], 0.9999)
     emit({"config": 5, "what": "f32 vs f64 DS projection sweep at the optimum",
           "points": n, "mask_disagreements": int((st64 != st32).sum()),
-          "max_rel_err_f32": float(rel)})
+          "max_rel_err_f32": float(d[i]), "p9999_rel_err_f32": float(q),
+          "worst": {"xyz": xyz[i].tolist(), "uv64": uv64[i].tolist(),
+                    "uv32": uv32[i].tolist()}, "ds_params": ds.params()})
 
 
 def main():
