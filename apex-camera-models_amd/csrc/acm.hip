@@ -321,18 +321,44 @@ __global__ __launch_bounds__(kBlock) void k_sum_columns(const double* __restrict
 }
 
 // ---------------------------------------------------- normal equations
-// acc layout: [upper triangle of JtJ (P(P+1)/2) | Jtr (P) | sum r.r | n_valid]
+// Every model's Jacobian rows have the same structure (camera_models.hpp):
+//   u-row [a, 0, 1, 0, du_0 .. du_{D-1}],  v-row [0, b, 0, 1, dv_0 .. dv_{D-1}]
+// with D = P - 4 distortion parameters.  J^T J therefore has structural
+// zeros ((fx,fy), (fx,cy), (fy,cx), (cx,cy)), (cx,cx) = (cy,cy) = n_valid,
+// and J^T r has r0 / r1 sums for cx / cy.  Accumulating only the non-trivial
+// sums (10 + 5D + D(D+1)/2 doubles per lane instead of P(P+1)/2 + P + 2)
+// cuts both the FMAs and the accumulator registers; for finite values the
+// sums are bit-identical to the dense ones (the dropped terms are exact 0).
+// acc layout:
+//   [0]        sum a^2        [1] sum a        [2, 2+D)      sum a du_k
+//   [2+D]      sum b^2        [3+D] sum b      [4+D, 4+2D)   sum b dv_k
+//   [4+2D, 4+3D) sum du_k     [4+3D, 4+4D)     sum dv_k
+//   [4+4D, 4+4D+DD) sum du_j du_k + dv_j dv_k (j <= k, DD = D(D+1)/2)
+//   then Jtr: sum a r0, sum b r1, sum r0, sum r1, sum du_k r0 + dv_k r1 (D)
+//   then sum r.r, n_valid
 template <int P>
 struct NE {
-    static constexpr int T = P * (P + 1) / 2;
-    static constexpr int K = T + P + 2;
+    static constexpr int D = P - 4;
+    static constexpr int DD = D * (D + 1) / 2;
+    static constexpr int A_DU = 2, B2 = 2 + D, B1 = 3 + D, B_DV = 4 + D;
+    static constexpr int DU = 4 + 2 * D, DV = 4 + 3 * D, DDB = 4 + 4 * D;
+    static constexpr int G = DDB + DD;  // Jtr block
+    static constexpr int K = G + 4 + D + 2;
 };
 
-constexpr int kNeMaxBlocks = 1024;
+constexpr int kNeMaxBlocks = 1024;  // reprojection stats / median partials
+constexpr int kNqMaxBlocks = 2048;  // normal equations: 8 workgroups per CU
 
 static int ne_blocks(size_t n) {
     size_t b = (n + kBlock - 1) / kBlock;
     if (b > (size_t)kNeMaxBlocks) b = kNeMaxBlocks;
+    if (b == 0) b = 1;
+    return (int)b;
+}
+
+static int nq_blocks(size_t n) {
+    size_t b = (n + kBlock - 1) / kBlock;
+    if (b > (size_t)kNqMaxBlocks) b = kNqMaxBlocks;
     if (b == 0) b = 1;
     return (int)b;
 }
@@ -344,52 +370,97 @@ __global__ __launch_bounds__(kBlock) void k_normal_eq(acm_camera cam, size_t n,
                                                       double* __restrict__ parts) {
     using M = typename TagT::template type<double>;
     constexpr int P = M::P;
-    constexpr int K = NE<P>::K;
+    using L = NE<P>;
+    constexpr int D = L::D;
+    constexpr int K = L::K;
     const Cam<double> c = make_cam<double>(cam);
     double acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
     const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
     const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        double x, y, z;
+    size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    // software pipeline: the next point's 40 bytes are in flight while the
+    // current one is projected and accumulated
+    double x = 0, y = 0, z = 1;
+    double2 o = make_double2(0.0, 0.0);
+    if (i < n) {
         load_point<LAYOUT>(pts, n, i, x, y, z);
-        const double2 o = *reinterpret_cast<const double2*>(obs + 2 * i);
+        o = *reinterpret_cast<const double2*>(obs + 2 * i);
+    }
+    for (; i < n; i += stride) {
+        const size_t inext = i + stride;
+        double xn = 0, yn = 0, zn = 1;
+        double2 on = make_double2(0.0, 0.0);
+        if (inext < n) {
+            load_point<LAYOUT>(pts, n, inext, xn, yn, zn);
+            on = *reinterpret_cast<const double2*>(obs + 2 * inext);
+        }
         double u, v, ju[P], jv[P];
         const uint8_t st = M::template project<true>(c, x, y, z, u, v, ju, jv);
         if (st == ST_OK) {
             const double r0 = u - o.x, r1 = v - o.y;
-            int t = 0;
+            const double a = ju[0], b = jv[1];
+            acc[0] += a * a;
+            acc[1] += a;
+            acc[L::B2] += b * b;
+            acc[L::B1] += b;
 #pragma unroll
-            for (int a = 0; a < P; ++a) {
-#pragma unroll
-                for (int b = a; b < P; ++b) acc[t++] += ju[a] * ju[b] + jv[a] * jv[b];
+            for (int k = 0; k < D; ++k) {
+                acc[L::A_DU + k] += a * ju[4 + k];
+                acc[L::B_DV + k] += b * jv[4 + k];
+                acc[L::DU + k] += ju[4 + k];
+                acc[L::DV + k] += jv[4 + k];
             }
+            int t = L::DDB;
 #pragma unroll
-            for (int a = 0; a < P; ++a) acc[NE<P>::T + a] += ju[a] * r0 + jv[a] * r1;
+            for (int j = 0; j < D; ++j) {
+#pragma unroll
+                for (int k = j; k < D; ++k) acc[t++] += ju[4 + j] * ju[4 + k] + jv[4 + j] * jv[4 + k];
+            }
+            acc[L::G + 0] += a * r0;
+            acc[L::G + 1] += b * r1;
+            acc[L::G + 2] += r0;
+            acc[L::G + 3] += r1;
+#pragma unroll
+            for (int k = 0; k < D; ++k) acc[L::G + 4 + k] += ju[4 + k] * r0 + jv[4 + k] * r1;
             acc[K - 2] += r0 * r0 + r1 * r1;
             acc[K - 1] += 1.0;
         } else {
             acc[K - 2] += sent2;
         }
+        x = xn; y = yn; z = zn; o = on;
     }
     block_sum_store<K>(acc, parts + (size_t)blockIdx.x * K);
 }
 
-// expand [tri | Jtr | rr | nv] -> [JtJ full (P*P) | Jtr | 0.5*rr | nv]
-__global__ void k_ne_expand(const double* __restrict__ sums, int P, double* __restrict__ out) {
-    const int T = P * (P + 1) / 2;
+// expand the structured sums -> [JtJ full (P*P) | Jtr (P) | 0.5*rr | n_valid]
+template <int P>
+__global__ void k_ne_expand(const double* __restrict__ s, double* __restrict__ out) {
+    using L = NE<P>;
+    constexpr int D = L::D;
     if (threadIdx.x != 0) return;
-    int t = 0;
-    for (int a = 0; a < P; ++a)
-        for (int b = a; b < P; ++b) {
-            out[a * P + b] = sums[t];
-            out[b * P + a] = sums[t];
-            ++t;
-        }
-    for (int a = 0; a < P; ++a) out[P * P + a] = sums[T + a];
-    out[P * P + P] = 0.5 * sums[T + P];
-    out[P * P + P + 1] = sums[T + P + 1];
+    for (int q = 0; q < P * P; ++q) out[q] = 0.0;
+    const double nv = s[L::K - 1];
+    auto set = [&](int r, int c, double v) { out[r * P + c] = v; out[c * P + r] = v; };
+    set(0, 0, s[0]);
+    set(0, 2, s[1]);
+    set(1, 1, s[L::B2]);
+    set(1, 3, s[L::B1]);
+    set(2, 2, nv);
+    set(3, 3, nv);
+    for (int k = 0; k < D; ++k) {
+        set(0, 4 + k, s[L::A_DU + k]);
+        set(1, 4 + k, s[L::B_DV + k]);
+        set(2, 4 + k, s[L::DU + k]);
+        set(3, 4 + k, s[L::DV + k]);
+    }
+    int t = L::DDB;
+    for (int j = 0; j < D; ++j)
+        for (int k = j; k < D; ++k) set(4 + j, 4 + k, s[t++]);
+    for (int q = 0; q < 4 + D; ++q) out[P * P + q] = s[L::G + q];
+    out[P * P + P] = 0.5 * s[L::K - 2];
+    out[P * P + P + 1] = nv;
 }
 
 // ----------------------------------------------------- reprojection stats
@@ -1192,8 +1263,9 @@ ACM_API int acm_residual_jacobian(const acm_camera* cam, size_t n, const double*
 ACM_API size_t acm_normal_equations_workspace_size(int model, size_t n) {
     const int P = acm_num_params(model);
     if (P < 0) return 0;
-    const int K = P * (P + 1) / 2 + P + 2;
-    return ((size_t)ne_blocks(n) + 1) * (size_t)K * sizeof(double);
+    const int D = P - 4;
+    const int K = 10 + 5 * D + D * (D + 1) / 2 + 2;  // = NE<P>::K
+    return ((size_t)nq_blocks(n) + 1) * (size_t)K * sizeof(double);
 }
 
 ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* points_3d,
@@ -1210,7 +1282,7 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
     if (workspace_bytes < acm_normal_equations_workspace_size(cam->model, n))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "normal-equations workspace too small");
     hipStream_t s = (hipStream_t)stream;
-    const int nb = ne_blocks(n);
+    const int nb = nq_blocks(n);
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
         using M = typename TagT::template type<double>;
@@ -1225,7 +1297,7 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
             hipLaunchKernelGGL((k_normal_eq<TagT, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s,
                                prep(*cam), n, points_3d, points_2d_obs, invalid_policy, parts);
         hipLaunchKernelGGL(k_sum_columns, dim3(K), dim3(kBlock), 0, s, parts, nb, K, sums);
-        hipLaunchKernelGGL(k_ne_expand, dim3(1), dim3(64), 0, s, sums, P, result);
+        hipLaunchKernelGGL(k_ne_expand<P>, dim3(1), dim3(64), 0, s, sums, result);
         return check_launch("acm_normal_equations");
     });
 }

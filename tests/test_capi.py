@@ -112,7 +112,8 @@ def test_sample_grid_matches_reference_formula(w, h, n):
 def test_workspace_sizes():
     from apex_camera_models import _lib
     L = _lib.load()
-    K = 8 * 9 // 2 + 8 + 2
-    assert L.acm_normal_equations_workspace_size(2, 10_000_000) == (1024 + 1) * K * 8
+    D = 8 - 4  # KB: structured normal-equation sums, 10 + 5D + D(D+1)/2 + 2
+    K = 10 + 5 * D + D * (D + 1) // 2 + 2
+    assert L.acm_normal_equations_workspace_size(2, 10_000_000) == (2048 + 1) * K * 8
     assert L.acm_reprojection_stats_workspace_size(1000) >= 1000 * 8
     assert L.acm_median_workspace_size(10) > 0

@@ -112,6 +112,32 @@ def config3(n_target):
           "initial_mean_px": met.initial_reprojection_error.mean})
 
 
+def config3_ne_all(n):
+    """Fused normal equations for every model on the same synthetic batch."""
+    import torch
+    from apex_camera_models import factors, samples
+    from apex_camera_models.camera import MODEL_CLASSES, Resolution
+    pts = samples.synthetic_points_device(n)
+    pts = pts[torch.isfinite(pts).all(1)].contiguous()
+    n = pts.shape[0]
+    facs = [factors.PinholeCameraParamsFactor, factors.RadTanCameraParamsFactor,
+            factors.KannalaBrandtCameraParamsFactor, factors.DoubleSphereCameraParamsFactor,
+            factors.UcmCameraParamsFactor, factors.EucmCameraParamsFactor,
+            factors.FovCameraParamsFactor]
+    for mid, fcls in enumerate(facs):
+        params, (w, h) = samples.SAMPLES[mid]
+        m = fcls.MODEL._from_params(list(params), Resolution(w, h))
+        uv, _, _ = m.project_batch(pts)
+        obs = torch.nan_to_num(uv, nan=0.0) + 0.25
+        f = fcls(pts, obs, Resolution(w, h))
+        P = len(params)
+        out = torch.empty((P * P + P + 2,), dtype=torch.float64, device="cuda")
+        ms = timed(lambda: f.normal_equations(params, out))
+        emit({"config": 3, "what": "fused normal equations", "model": fcls.MODEL.__name__,
+              "points": n, "ms": round(ms, 4), "Mpoints_per_s": round(n / ms / 1e3, 1),
+              "GBps": round(40 * n / ms / 1e6, 1)})
+
+
 def config4(n_per_model):
     """Every model: project -> unproject round trip (two launches, uv
     intermediate in HBM), plus the round-trip error sum (RCCL all-reduce on
@@ -204,6 +230,8 @@ def main():
         config1()
     if "3" in cs:
         config3(int(10_000_000 * a.scale))
+    if "3ne" in cs:
+        config3_ne_all(int(10_000_000 * a.scale))
     if "4" in cs:
         config4(int(6_250_000 * a.scale))
     if "5" in cs:
