@@ -34,6 +34,17 @@ enum : uint8_t {
 constexpr double kEps = 2.220446049250313e-16;      // f64::EPSILON
 constexpr double kEpsSqrt = 1.4901161193847656e-08;  // f64::EPSILON.sqrt()
 constexpr double kPi = 3.141592653589793;
+// Smallest double s with sqrt(s) >= 1e-6 under correctly rounded sqrt, so
+// `sqrt(s) < 1e-6` == `s < kNewtonTol2` for every s >= 0 (and both are false
+// for NaN).  Lets the RadTan Newton loop drop two sqrt per step with the
+// reference's decisions unchanged bit for bit (tests/test_capi.py pins it).
+constexpr double kNewtonTol2 = 0x1.19799812dea10p-40;
+
+template <class T>
+__device__ __forceinline__ bool norm_below_1e6(T sq) {
+    if constexpr (sizeof(T) == 8) return sq < T(kNewtonTol2);
+    else return sqrt(sq) < T(1e-6);
+}
 
 // Uniform camera parameters, converted once per thread from the kernel
 // argument (they stay in SGPRs: every lane reads the same values).
@@ -132,7 +143,6 @@ struct RadTan {
         const T tx = (u - cx) / fx;
         const T ty = (v - cy) / fy;
         T px = tx, py = ty;
-        const T EPS = T(1e-6);
         uint8_t st = ST_OK;
         for (unsigned it = 0; it < 100u; ++it) {
             T x = px, y = py;
@@ -149,7 +159,7 @@ struct RadTan {
             // keeps NaN/inf pixels (0.1% of the bench cloud) from holding
             // their whole wave for 100 iterations.
             if (ex != ex || ey != ey) { st = ST_NUMERICAL_ERROR; break; }
-            if (sqrt(ex * ex + ey * ey) < EPS) break;  // :459
+            if (norm_below_1e6(ex * ex + ey * ey)) break;  // :459, sqrt(.) < EPS
             T drdx = T(2) * x, drdy = T(2) * y;
             T ddx = (k1 + T(2) * k2 * r2 + T(3) * k3 * r4) * drdx;
             T ddy = (k1 + T(2) * k2 * r2 + T(3) * k3 * r4) * drdy;
@@ -166,7 +176,7 @@ struct RadTan {
             T dy = i10 * ex + i11 * ey;
             px = px - dx;
             py = py - dy;
-            if (sqrt(dx * dx + dy * dy) < EPS) break;  // :503
+            if (norm_below_1e6(dx * dx + dy * dy)) break;  // :503, sqrt(.) < EPS
             if (it == 99u) st = ST_NUMERICAL_ERROR;    // :514
         }
         T n = sqrt(px * px + py * py + T(1) * T(1));
