@@ -77,6 +77,8 @@ class AcmCamera(ctypes.Structure):
     ]
 
 
+FOV_GRID_SIZE = 290  # ACM_FOV_GRID_SIZE
+
 EXPORTED_SYMBOLS = (
     "acm_num_params",
     "acm_camera_init",
@@ -94,6 +96,9 @@ EXPORTED_SYMBOLS = (
     "acm_linear_system_qr",
     "acm_linear_estimation_workspace_size",
     "acm_linear_estimation",
+    "acm_fov_grid_workspace_size",
+    "acm_fov_grid_errors",
+    "acm_fov_grid_select",
     "acm_lm_default_config",
     "acm_lm_workspace_size",
     "acm_lm_optimize",
@@ -182,6 +187,12 @@ def load():
     L.acm_linear_estimation_workspace_size.restype = sz
     L.acm_linear_estimation.argtypes = [cam_p, sz, vp, i, vp, vp, sz, vp]
     L.acm_linear_estimation.restype = i
+    L.acm_fov_grid_workspace_size.argtypes = [sz]
+    L.acm_fov_grid_workspace_size.restype = sz
+    L.acm_fov_grid_errors.argtypes = [cam_p, sz, vp, i, vp, vp, vp, sz, vp]
+    L.acm_fov_grid_errors.restype = i
+    L.acm_fov_grid_select.argtypes = [cam_p, ctypes.POINTER(ctypes.c_double)]
+    L.acm_fov_grid_select.restype = i
     L.acm_lm_default_config.argtypes = [ctypes.POINTER(LmConfig)]
     L.acm_lm_default_config.restype = None
     L.acm_lm_workspace_size.argtypes = [i, sz]

@@ -9,8 +9,8 @@ import time
 from dataclasses import dataclass
 
 from . import util
-from .camera import (CameraModel, DoubleSphereModel, EucmModel, Intrinsics, KannalaBrandtModel,
-                     RadTanModel, UcmModel)
+from .camera import (CameraModel, DoubleSphereModel, EucmModel, FovModel, Intrinsics,
+                     KannalaBrandtModel, RadTanModel, UcmModel)
 from .optimizer import CONVERTER_BOUNDS, LevenbergMarquardt, LevenbergMarquardtConfig
 
 
@@ -27,7 +27,7 @@ class ConversionMetrics:
 
 
 # initial target parameters (camera_converter.rs:364-369, :500-505, :639-644,
-# :781-785, :911-916)
+# :781-785, :911-916, :1045-1049)
 def _init_target(name, src: CameraModel):
     i = src.get_intrinsics()
     res = src.get_resolution()
@@ -42,12 +42,14 @@ def _init_target(name, src: CameraModel):
         return UcmModel(intr, res, 0.5)
     if name == "eucm":
         return EucmModel(intr, res, 0.5, 1.0)
+    if name == "fov":
+        return FovModel(intr, res, 1.0)
     raise ValueError(name)
 
 
 DISPLAY = {"double_sphere": "Double Sphere", "kannala_brandt": "Kannala-Brandt",
            "rad_tan": "Radial-Tangential", "ucm": "Unified Camera Model",
-           "eucm": "Extended Unified Camera Model"}
+           "eucm": "Extended Unified Camera Model", "fov": "Field-of-View"}
 
 
 def convert(input_model: CameraModel, target: str, points_3d, points_2d,
@@ -81,8 +83,9 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
 
 
 def convert_all(input_model: CameraModel, num_points: int = 500,
-                targets=("double_sphere", "kannala_brandt", "rad_tan", "ucm", "eucm")):
+                targets=("double_sphere", "kannala_brandt", "rad_tan", "ucm", "eucm", "fov")):
     """camera_converter.rs main (:127-350): sample_points once (:189), then
-    every target conversion."""
+    every target conversion except the input's own model (:225-340)."""
     points_2d, points_3d = util.sample_points(input_model, num_points)
-    return {t: convert(input_model, t, points_3d, points_2d) for t in targets}
+    return {t: convert(input_model, t, points_3d, points_2d) for t in targets
+            if t != input_model.NAME}

@@ -17,6 +17,7 @@
 //     result is bit-reproducible run to run.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -963,6 +964,83 @@ __global__ __launch_bounds__(kBlock) void k_tsqr_final(const double* __restrict_
     }
 }
 
+// ------------------------------------------------------- FOV grid search
+// fov.rs:153-251: FOV's linear_estimation is a grid search -- for each
+// w = i/100 (i = 10..299) the mean reprojection error of a simplified FOV
+// projection over all points.  Here each lane owns ONE grid value (290 lanes
+// of a 320-lane workgroup) and walks a contiguous chunk of points staged in
+// LDS (every lane reads the same point: broadcast, no bank conflicts), so
+// its running sum follows the reference's serial point order within the
+// chunk and no cross-lane reduction is needed.  The per-w constants come
+// from a host-built table (w, 2 tan(w/2), 2 tan(w/2)/w) so tan is glibc's.
+// Compute-bound: one f64 atan2 + 2 div + sqrt per (point, w).
+constexpr int kFovGrid = ACM_FOV_GRID_SIZE;
+constexpr int kFovBlock = 320;
+constexpr int kFovMaxBlocks = 2048;
+
+template <int LAYOUT>
+__global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n, size_t chunk,
+                                                        const double* __restrict__ pts,
+                                                        const double* __restrict__ obs,
+                                                        const double* __restrict__ table,
+                                                        double* __restrict__ parts) {
+    __shared__ double sx[kFovBlock], sy[kFovBlock], sz[kFovBlock], su[kFovBlock],
+        sv[kFovBlock], sr2[kFovBlock], sr[kFovBlock];
+    const int t = threadIdx.x;
+    const bool active = t < kFovGrid;
+    const double fx = cam.params[0], fy = cam.params[1], cx = cam.params[2], cy = cam.params[3];
+    double w = 1.0, tw2 = 0.0, rd0 = 0.0;
+    if (active) {
+        w = table[3 * t];
+        tw2 = table[3 * t + 1];
+        rd0 = table[3 * t + 2];
+    }
+    const size_t b0 = (size_t)blockIdx.x * chunk;
+    const size_t b1 = b0 + chunk < n ? b0 + chunk : n;
+    double sum = 0.0, cnt = 0.0;
+    for (size_t base = b0; base < b1; base += kFovBlock) {
+        __syncthreads();
+        const size_t i = base + t;
+        if (i < b1) {
+            double x, y, z;
+            load_point<LAYOUT>(pts, n, i, x, y, z);
+            const double r2 = x * x + y * y;  // :192-193
+            sx[t] = x; sy[t] = y; sz[t] = z;
+            su[t] = obs[2 * i]; sv[t] = obs[2 * i + 1];
+            sr2[t] = r2; sr[t] = sqrt(r2);
+        }
+        __syncthreads();
+        const int m = (int)(b1 - base < (size_t)kFovBlock ? b1 - base : (size_t)kFovBlock);
+        if (active) {
+            for (int k = 0; k < m; ++k) {
+                const double x = sx[k], y = sy[k], r2 = sr2[k];
+                double rd;
+                if (r2 < kEpsSqrt) rd = rd0;  // :200-205 (uniform over the wave)
+                else rd = atan2(tw2 * sr[k], sz[k]) / (sr[k] * w);
+                const double mx = x * rd, my = y * rd;
+                const double du = (fx * mx + cx) - su[k];
+                const double dv = (fy * my + cy) - sv[k];
+                const double e = sqrt(du * du + dv * dv);  // :211-213
+                if (isfinite(e)) { sum += e; cnt += 1.0; }
+            }
+        }
+    }
+    if (active) {
+        parts[(size_t)blockIdx.x * (2 * kFovGrid) + t] = sum;
+        parts[(size_t)blockIdx.x * (2 * kFovGrid) + kFovGrid + t] = cnt;
+    }
+}
+
+// Chunk sums combined in block order (deterministic), one lane per column.
+__global__ __launch_bounds__(kBlock) void k_fov_finish(const double* __restrict__ parts, int nb,
+                                                       double* __restrict__ out) {
+    const int c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= 2 * kFovGrid) return;
+    double s = 0.0;
+    for (int b = 0; b < nb; ++b) s += parts[(size_t)b * (2 * kFovGrid) + c];
+    out[c] = s;
+}
+
 // ---------------------------------------------------------- undistort_image
 // undistort.rs:14-105: per output pixel, the ray ((u-cx')/fx', (v-cy')/fy', 1)
 // of the target intrinsics is projected through the camera model and the
@@ -1471,6 +1549,64 @@ ACM_API int acm_linear_system_qr(const acm_camera* cam, size_t n, const double* 
     default: go(std::integral_constant<int, ACM_EUCM>{}); break;
     }
     return check_launch("acm_linear_system_qr");
+}
+
+// FOV linear_estimation grid (fov.rs:153-251); the selection is host code
+// in solver.hip (acm_fov_grid_select).
+static size_t fov_blocks(size_t n) {
+    size_t nb = (n + kBlock - 1) / kBlock;  // >= 256 points per chunk
+    if (nb > (size_t)kFovMaxBlocks) nb = kFovMaxBlocks;
+    return nb ? nb : 1;
+}
+
+static const double* fov_grid_table() {
+    static double table[3 * kFovGrid];
+    static const bool init = [] {
+        for (int i = 10; i < 10 + kFovGrid; ++i) {
+            const double w = (double)i / 100.0;          // :180
+            const double tan_w_half = std::tan(w / 2.0);  // :195
+            table[3 * (i - 10)] = w;
+            table[3 * (i - 10) + 1] = 2.0 * tan_w_half;          // :196, exact
+            table[3 * (i - 10) + 2] = 2.0 * tan_w_half / w;      // :202
+        }
+        return true;
+    }();
+    (void)init;
+    return table;
+}
+
+ACM_API size_t acm_fov_grid_workspace_size(size_t n) {
+    return (fov_blocks(n) * 2 * kFovGrid + 3 * kFovGrid) * sizeof(double);
+}
+
+ACM_API int acm_fov_grid_errors(const acm_camera* cam, size_t n, const double* points_3d,
+                                int layout, const double* points_2d, double* grid_sums,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if ((rc = check_layout(layout))) return rc;
+    if (cam->model != ACM_FOV) return fail(ACM_ERR_NOT_SUPPORTED, "grid search is FOV-only");
+    if (!grid_sums || !workspace || (n && (!points_3d || !points_2d)))
+        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_fov_grid_workspace_size(n))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "FOV grid workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t nb = fov_blocks(n);
+    const size_t chunk = (n + nb - 1) / nb;
+    double* parts = (double*)workspace;
+    double* table = parts + nb * 2 * kFovGrid;
+    if (hipMemcpyAsync(table, fov_grid_table(), 3 * kFovGrid * sizeof(double),
+                       hipMemcpyHostToDevice, s) != hipSuccess)
+        return check_launch("acm_fov_grid_errors (table)");
+    if (layout == ACM_LAYOUT_AOS)
+        hipLaunchKernelGGL((k_fov_grid<ACM_LAYOUT_AOS>), dim3(nb), dim3(kFovBlock), 0, s, *cam, n,
+                           chunk, points_3d, points_2d, table, parts);
+    else
+        hipLaunchKernelGGL((k_fov_grid<ACM_LAYOUT_SOA>), dim3(nb), dim3(kFovBlock), 0, s, *cam, n,
+                           chunk, points_3d, points_2d, table, parts);
+    hipLaunchKernelGGL(k_fov_finish, dim3((2 * kFovGrid + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       s, parts, (int)nb, grid_sums);
+    return check_launch("acm_fov_grid_errors");
 }
 
 ACM_API size_t acm_median_workspace_size(size_t n) {

@@ -108,11 +108,56 @@ int validate(const acm_camera* cam) {
     return sfail(ACM_ERR_INVALID_PARAMS, "validate_params failed after linear estimation");
 }
 
+int fov_linear_estimation(acm_camera* cam, size_t n, const double* points_3d, int layout,
+                          const double* points_2d, void* workspace, size_t workspace_bytes,
+                          void* stream) {
+    if (n < 2)  // fov.rs:166-171
+        return sfail(ACM_ERR_INVALID_PARAMS,
+                     "Need at least 2 point correspondences for linear estimation");
+    const size_t g = acm_fov_grid_workspace_size(n);
+    if (!workspace || workspace_bytes < g + 2 * ACM_FOV_GRID_SIZE * sizeof(double))
+        return sfail(ACM_ERR_WORKSPACE_TOO_SMALL, "linear-estimation workspace too small");
+    double* d_sums = (double*)((char*)workspace + g);
+    int rc = acm_fov_grid_errors(cam, n, points_3d, layout, points_2d, d_sums, workspace, g,
+                                 stream);
+    if (rc) return rc;
+    double sums[2 * ACM_FOV_GRID_SIZE];
+    hipStream_t s = (hipStream_t)stream;
+    if (hip_ok(hipMemcpyAsync(sums, d_sums, sizeof(sums), hipMemcpyDeviceToHost, s)) ||
+        hip_ok(hipStreamSynchronize(s)))
+        return sfail(ACM_ERR_HIP, "FOV grid search: device copy failed");
+    return acm_fov_grid_select(cam, sums);
+}
+
 }  // namespace
 
 extern "C" {
 
+// fov.rs:176-249: first grid value with the strictly smallest mean error
+// (best starts at w = 1.0, +inf), then the clamp and validate_params.
+ACM_API int acm_fov_grid_select(acm_camera* cam, const double* grid_sums_host) {
+    if (!cam || !grid_sums_host) return sfail(ACM_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (cam->model != ACM_FOV) return sfail(ACM_ERR_NOT_SUPPORTED, "grid search is FOV-only");
+    double best_w = 1.0, best_error = INFINITY;
+    for (int i = 0; i < ACM_FOV_GRID_SIZE; ++i) {
+        const double cnt = grid_sums_host[ACM_FOV_GRID_SIZE + i];
+        if (cnt > 0.0) {
+            const double avg = grid_sums_host[i] / cnt;
+            if (avg < best_error) {
+                best_error = avg;
+                best_w = (double)(i + 10) / 100.0;
+            }
+        }
+    }
+    if (best_w <= 2.220446049250313e-16) best_w = 0.01;  // :236-242
+    else if (best_w > 3.0) best_w = 3.0;
+    cam->params[4] = best_w;
+    return validate(cam);
+}
+
 ACM_API size_t acm_linear_estimation_workspace_size(int model, size_t n) {
+    if (model == ACM_FOV)
+        return acm_fov_grid_workspace_size(n) + 2 * ACM_FOV_GRID_SIZE * sizeof(double);
     const size_t qr = acm_linear_system_qr_workspace_size(model, n);
     if (!qr) return 0;
     return qr + 32 * sizeof(double);
@@ -124,6 +169,8 @@ ACM_API int acm_linear_estimation(acm_camera* cam, size_t n, const double* point
                                   const double* points_2d, void* workspace,
                                   size_t workspace_bytes, void* stream) {
     if (!cam) return sfail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
+    if (cam->model == ACM_FOV) return fov_linear_estimation(cam, n, points_3d, layout, points_2d,
+                                                            workspace, workspace_bytes, stream);
     const int k = acm_linear_system_columns(cam->model);
     if (k < 0) return sfail(ACM_ERR_NOT_SUPPORTED, "model has no linear_estimation");
     if (cam->model == ACM_KANNALA_BRANDT && n < 4)  // :174-178

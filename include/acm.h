@@ -192,7 +192,7 @@ ACM_API int acm_reprojection_stats(const acm_camera *cam, size_t n,
  * solves R_A x = z on the host with nalgebra's SVD::solve(eps) semantics
  * (eps = f64::EPSILON for KB, 1e-10 otherwise), applies the model's clamps
  * and validation, and writes the estimate into cam->params (k = 4 KB,
- * 3 RadTan, 1 DS/UCM/EUCM; FOV's grid search is not supported). */
+ * 3 RadTan, 1 DS/UCM/EUCM; FOV: the grid search below). */
 ACM_API int acm_linear_system_columns(int model);
 ACM_API size_t acm_linear_system_qr_workspace_size(int model, size_t n);
 ACM_API int acm_linear_system_qr(const acm_camera *cam, size_t n,
@@ -205,6 +205,25 @@ ACM_API int acm_linear_estimation(acm_camera *cam, size_t n,
                                   const double *points_3d, int layout,
                                   const double *points_2d, void *workspace,
                                   size_t workspace_bytes, void *stream);
+
+/* FOV linear_estimation (fov.rs:153-251) is a grid search, not a linear
+ * system: for w = i/100, i = 10..299 (ACM_FOV_GRID_SIZE values) the sum of
+ * finite reprojection errors and their count over all points.
+ * acm_fov_grid_errors writes grid_sums (device, 2 x 290 doubles: the 290
+ * error sums, then the 290 counts); the sums are additive over shards of
+ * the points, so a multi-GPU caller all-reduces them before
+ * acm_fov_grid_select, which keeps the first w with the strictly smallest
+ * mean (host array), applies the clamp to [0.01, 3] and validate_params,
+ * and writes w into cam->params[4].  acm_linear_estimation runs both for
+ * ACM_FOV (n < 2 -> ACM_ERR_INVALID_PARAMS, fov.rs:166-171). */
+#define ACM_FOV_GRID_SIZE 290
+ACM_API size_t acm_fov_grid_workspace_size(size_t n);
+ACM_API int acm_fov_grid_errors(const acm_camera *cam, size_t n,
+                                const double *points_3d, int layout,
+                                const double *points_2d, double *grid_sums,
+                                void *workspace, size_t workspace_bytes,
+                                void *stream);
+ACM_API int acm_fov_grid_select(acm_camera *cam, const double *grid_sums_host);
 
 /* Bounded Levenberg-Marquardt over the fused normal equations: the
  * apex-solver call of camera_converter.rs:381-420.  Each evaluation runs

@@ -65,6 +65,8 @@ def lib():
         L.oracle_sample_points.restype = sz
         L.oracle_linear_estimation_system.argtypes = [ctypes.c_int, dp, sz, dp, dp, dp, dp]
         L.oracle_linear_estimation_system.restype = ctypes.c_int
+        L.oracle_fov_grid_search.argtypes = [dp, sz, dp, dp, dp, dp]
+        L.oracle_fov_grid_search.restype = ctypes.c_double
         L.oracle_undistort_image.argtypes = [ctypes.c_int, dp, u32, u32, dp, ctypes.c_int,
                                              u8p, u8p]
         L.oracle_undistort_image.restype = None
@@ -182,6 +184,22 @@ def linear_estimation_system(model, params, xyz, uv):
     if k < 0:
         return None, None, k
     return A.reshape(-1)[: 2 * n * k].reshape(2 * n, k).copy(), b, k
+
+
+def fov_grid_search(params, xyz, uv):
+    """FOV linear_estimation grid search (fov.rs:153-251).  Returns
+    (best_w or None if n < 2, error_sum (290,), valid_count (290,))."""
+    params = _f64(params)
+    xyz = _f64(xyz).reshape(-1, 3)
+    uv = _f64(uv).reshape(-1, 2)
+    s = np.zeros(290)
+    c = np.zeros(290)
+    w = lib().oracle_fov_grid_search(_dp(params), xyz.shape[0], _dp(xyz), _dp(uv), _dp(s),
+                                     _dp(c))
+    return (None if w < 0 else w), s, c
+
+
+FOV_GRID = np.arange(10, 300) / 100.0
 
 
 def undistort_image(model, params, w, h, target, bilinear, img):

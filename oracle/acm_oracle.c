@@ -697,6 +697,47 @@ size_t oracle_sample_points(int model, const double *params, uint32_t w,
     return m;
 }
 
+/* ------------------------------------------------------ FOV grid search */
+/* src/camera/fov.rs:153-251, statement for statement: for each grid w the
+ * points are visited in order and every finite error is added to a running
+ * sum; the first w with the strictly smallest average wins. */
+double oracle_fov_grid_search(const double *params, size_t n, const double *xyz,
+                              const double *uv, double *error_sum,
+                              double *valid_count) {
+    const double fx = params[0], fy = params[1], cx = params[2], cy = params[3];
+    double best_w = 1.0, best_error = INFINITY;
+    for (int i = 10; i < 300; ++i) { /* :180 */
+        const double w_test = (double)i / 100.0;
+        double sum = 0.0;
+        size_t cnt = 0;
+        for (size_t k = 0; k < n; ++k) {
+            const double x = xyz[3 * k], y = xyz[3 * k + 1], z = xyz[3 * k + 2];
+            const double uo = uv[2 * k], vo = uv[2 * k + 1];
+            const double r2 = x * x + y * y;                      /* :192 */
+            const double r = sqrt(r2);
+            const double tan_w_half = tan(w_test / 2.0);          /* :195 */
+            const double atan_wrd = atan2(2.0 * tan_w_half * r, z);
+            const double eps_sqrt = sqrt(DBL_EPSILON);            /* :198 */
+            const double rd = r2 < eps_sqrt ? 2.0 * tan_w_half / w_test
+                                            : atan_wrd / (r * w_test);
+            const double mx = x * rd, my = y * rd;
+            const double up = fx * mx + cx, vp = fy * my + cy;    /* :208-209 */
+            const double du = up - uo, dv = vp - vo;
+            const double e = sqrt(du * du + dv * dv);             /* :211-213 */
+            if (isfinite(e)) { sum += e; ++cnt; }
+        }
+        error_sum[i - 10] = sum;
+        valid_count[i - 10] = (double)cnt;
+        if (cnt > 0) { /* :221-227 */
+            const double avg = sum / (double)cnt;
+            if (avg < best_error) { best_error = avg; best_w = w_test; }
+        }
+    }
+    /* :166-171 rejects n < 2 before searching; the sums are still filled so
+     * the GPU grid can be checked at n = 0 / 1 too. */
+    return n < 2 ? -1.0 : best_w;
+}
+
 /* -------------------------------------------------------- linear estimation */
 int oracle_linear_estimation_system(int model, const double *params, size_t n,
                                     const double *xyz, const double *uv,

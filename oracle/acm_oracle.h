@@ -112,6 +112,16 @@ int oracle_linear_estimation_system(int model, const double *params,
                                     size_t n, const double *xyz,
                                     const double *uv, double *A, double *b);
 
+/* FOV linear_estimation (src/camera/fov.rs:153-251): the grid search over
+ * w = i/100, i = 10..299.  Writes, per grid value, the serial error sum and
+ * the finite-error count (both 290 long), and returns the w the reference
+ * keeps (before its clamp / validate), or -1.0 if n < 2 (InvalidParams;
+ * the sums are filled in either case). */
+#define ORACLE_FOV_GRID 290
+double oracle_fov_grid_search(const double *params, size_t n, const double *xyz,
+                              const double *uv, double *error_sum,
+                              double *valid_count);
+
 /* undistort_image (src/util/undistort.rs:14-105): RGB8 row-major w x h,
  * target = [fx fy cx cy], bilinear 0 = Nearest, 1 = Bilinear. */
 void oracle_undistort_image(int model, const double *params, uint32_t w,

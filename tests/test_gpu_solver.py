@@ -194,3 +194,103 @@ def test_lm_rccl_allreduce_single_rank():
         assert a.lm_iterations == b.lm_iterations
     finally:
         dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- FOV
+FOV = 6
+
+
+def _fov_grid_gpu(params, xyz, uv, w=752, h=480):
+    import ctypes
+
+    import torch
+    from apex_camera_models import _lib
+    L = _lib.load()
+    m = _model(FOV, params, w, h)
+    cam = m.acm_camera()
+    p3 = torch.as_tensor(np.ascontiguousarray(xyz), dtype=torch.float64, device="cuda")
+    p2 = torch.as_tensor(np.ascontiguousarray(uv), dtype=torch.float64, device="cuda")
+    n = p3.shape[0]
+    ws_b = L.acm_fov_grid_workspace_size(n)
+    ws = torch.empty(((ws_b + 7) // 8,), dtype=torch.float64, device="cuda")
+    out = torch.full((2 * _lib.FOV_GRID_SIZE,), np.nan, dtype=torch.float64, device="cuda")
+    _lib.check(L.acm_fov_grid_errors(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
+                                     p2.data_ptr(), out.data_ptr(), ws.data_ptr(), ws_b, None))
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    return o[:290], o[290:]
+
+
+def _fov_data(n, seed, w_true=None, noise=0.0):
+    params, (w, h) = SAMPLES[FOV]
+    p = list(params[:4]) + [w_true if w_true is not None else params[4]]
+    rng = np.random.default_rng(seed)
+    xyz = np.stack([rng.uniform(-1, 1, n), rng.uniform(-1, 1, n), rng.uniform(0.5, 4.0, n)], 1)
+    if n > 8:
+        xyz[0] = [0.0, 0.0, 1.0]
+        xyz[1] = [0.2, -0.1, 0.0]
+        xyz[2] = [np.nan, 0.1, 1.0]
+        xyz[3] = [1e-9, 0.0, 2.0]
+    uv, _, _ = O.project(FOV, p, w, h, xyz)
+    uv = np.where(np.isnan(uv), 5.0, uv) + noise * rng.standard_normal(uv.shape)
+    return p, xyz, uv
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 257, 320 * 3 + 5, 20_000])
+def test_fov_grid_errors_match_oracle(n):
+    p, xyz, uv = _fov_data(n, 40 + n, noise=0.7)
+    bw, s_ref, c_ref = O.fov_grid_search(p, xyz, uv)
+    s, c = _fov_grid_gpu(p, xyz, uv)
+    assert np.array_equal(c, c_ref)  # counts exact
+    # sums: same terms, chunked summation order and OCML atan2 -> 1e-12 rel
+    assert np.all(np.abs(s - s_ref) <= 1e-12 * np.abs(s_ref) + 1e-300)
+    if bw is not None:
+        avg = np.where(c > 0, s / np.maximum(c, 1), np.inf)
+        assert (np.argmin(avg) + 10) / 100.0 == bw
+
+
+@pytest.mark.parametrize("w_true", [0.37, 0.93, 1.5, 2.41])
+def test_fov_linear_estimation_matches_reference(w_true):
+    import torch
+    p, xyz, uv = _fov_data(5000, 7, w_true=w_true)
+    bw, _, _ = O.fov_grid_search(p[:4] + [1.0], xyz, uv)
+    assert bw == w_true
+    m = _model(FOV, p[:4] + [1.0], 752, 480)
+    m.linear_estimation(torch.as_tensor(xyz), torch.as_tensor(uv))
+    assert m.w == w_true and m.params()[:4] == p[:4]
+    # noisy data: the same grid value as the serial reference loop
+    p, xyz, uv = _fov_data(5000, 8, w_true=w_true + 0.004, noise=0.5)
+    bw, _, _ = O.fov_grid_search(p[:4] + [1.0], xyz, uv)
+    m = _model(FOV, p[:4] + [1.0], 752, 480)
+    m.linear_estimation(torch.as_tensor(xyz), torch.as_tensor(uv))
+    assert m.w == bw
+
+
+def test_fov_linear_estimation_errors_and_shards():
+    import torch
+    from apex_camera_models.camera import InvalidParams
+    p, xyz, uv = _fov_data(1, 3)
+    m = _model(FOV, p, 752, 480)
+    with pytest.raises(InvalidParams):  # fov.rs:166-171
+        m.linear_estimation(torch.as_tensor(xyz), torch.as_tensor(uv))
+    with pytest.raises(InvalidParams):  # :159-163
+        m.linear_estimation(torch.zeros((4, 3), dtype=torch.float64),
+                            torch.zeros((3, 2), dtype=torch.float64))
+    # grid sums are additive over point shards (the multi-GPU all-reduce)
+    p, xyz, uv = _fov_data(9000, 9, noise=0.3)
+    s, c = _fov_grid_gpu(p, xyz, uv)
+    parts = [_fov_grid_gpu(p, xyz[a:b], uv[a:b]) for a, b in [(0, 3001), (3001, 6500),
+                                                               (6500, 9000)]]
+    assert np.array_equal(sum(q[1] for q in parts), c)
+    assert np.allclose(sum(q[0] for q in parts), s, rtol=1e-12, atol=0)
+
+
+def test_conversion_kb_to_fov():
+    from apex_camera_models import KannalaBrandtModel, Resolution, conversion, util
+    params, (w, h) = SAMPLES[KB]
+    src = KannalaBrandtModel._from_params(params, Resolution(w, h))
+    uv, xyz = util.sample_points(src, 500)
+    met = conversion.convert(src, "fov", xyz, uv)
+    assert met.model.NAME == "fov"
+    assert met.final_reprojection_error.mean <= met.initial_reprojection_error.mean
+    assert 1e-6 <= met.model.w <= 3.0

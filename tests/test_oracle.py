@@ -156,3 +156,66 @@ def test_rel_err_helper():
     assert rel_err([1.0, np.nan], [1.0, np.nan]) == 0.0
     with pytest.raises(AssertionError):
         rel_err([1.0, 2.0], [1.0, np.nan])
+
+
+def _py_fov_grid(params, xyz, uv):
+    """fov.rs:176-229 in plain Python floats (same IEEE ops, same libm)."""
+    import math
+    fx, fy, cx, cy = params[:4]
+    sums, cnts = [], []
+    best_w, best = 1.0, math.inf
+    for i in range(10, 300):
+        wt = i / 100.0
+        s, c = 0.0, 0
+        for (x, y, z), (uo, vo) in zip(xyz.tolist(), uv.tolist()):
+            r2 = x * x + y * y
+            r = math.sqrt(r2)
+            t = math.tan(wt / 2.0)
+            a = math.atan2(2.0 * t * r, z)
+            rd = 2.0 * t / wt if r2 < math.sqrt(2.220446049250313e-16) else a / (r * wt)
+            du = (fx * (x * rd) + cx) - uo
+            dv = (fy * (y * rd) + cy) - vo
+            e = math.sqrt(du * du + dv * dv)
+            if math.isfinite(e):
+                s += e
+                c += 1
+        sums.append(s)
+        cnts.append(c)
+        if c > 0 and s / c < best:
+            best, best_w = s / c, wt
+    return best_w, np.array(sums), np.array(cnts, dtype=float)
+
+
+def test_oracle_fov_grid_search_matches_python_restatement():
+    params, (w, h) = SAMPLES[6]
+    xyz = _rand_pts(60, 11)
+    xyz[0] = [0.0, 0.0, 1.0]       # r2 < sqrt(EPS) branch
+    xyz[1] = [0.3, 0.1, 0.0]       # z = 0
+    uv, _, _ = O.project(6, params, w, h, xyz)
+    uv = np.where(np.isnan(uv), np.inf, uv) + 0.3
+    uv[5] = [np.nan, 1.0]          # non-finite error -> skipped
+    bw, s, c = O.fov_grid_search(params[:4] + [1.0], xyz, uv)
+    pw, ps, pc = _py_fov_grid(params, xyz, uv)
+    assert bw == pw
+    assert np.array_equal(s, ps) and np.array_equal(c, pc)
+    assert c.max() <= 59
+
+
+@pytest.mark.parametrize("w_true", [0.37, 0.93, 1.5, 2.41])
+def test_oracle_fov_grid_recovers_on_grid_w(w_true):
+    # data projected by FovModel::project (fov.rs:284-316, the same formula as
+    # the search, :191-209) with an on-grid w has zero error exactly there
+    params, (w, h) = SAMPLES[6]
+    p = params[:4] + [w_true]
+    xyz = _rand_pts(300, 5)
+    uv, st, _ = O.project(6, p, w, h, xyz)
+    ok = st == 0
+    bw, s, c = O.fov_grid_search(p, xyz[ok], uv[ok])
+    assert bw == w_true
+    assert s[int(round(w_true * 100)) - 10] == 0.0
+
+
+def test_oracle_fov_grid_needs_two_points():
+    params, _ = SAMPLES[6]
+    bw, _, _ = O.fov_grid_search(params, np.zeros((1, 3)), np.zeros((1, 2)))
+    assert bw is None

@@ -139,6 +139,25 @@ def config3_ne_all(n):
               "GBps": round(40 * n / ms / 1e6, 1)})
 
 
+def config_fov(n_target):
+    """FOV linear_estimation (fov.rs:153-251 grid search, 290 x N evaluations)
+    on KB-sampled correspondences, then the full KB->FOV conversion."""
+    import torch
+    from apex_camera_models import KannalaBrandtModel, Resolution, conversion, samples, util
+    kp, (w, h) = samples.SAMPLES[2]
+    src = KannalaBrandtModel._from_params(kp, Resolution(w, h))
+    uv, xyz = util.sample_points(src, n_target)
+    n = xyz.shape[0]
+    m = conversion._init_target("fov", src)
+    ms = timed(lambda: m.linear_estimation(xyz, uv), reps=3, warm=1)
+    met = conversion.convert(src, "fov", xyz, uv)
+    emit({"config": "fov", "what": "FOV grid-search linear estimation", "points": n,
+          "ms": round(ms, 3), "evaluations_per_s": round(290 * n / ms / 1e3, 1), "w": m.w,
+          "convert_ms": round(met.optimization_time_ms, 2), "lm_iterations": met.lm_iterations,
+          "termination": met.lm_termination,
+          "final_mean_px": met.final_reprojection_error.mean})
+
+
 def config4(n_per_model):
     """Every model: project -> unproject round trip (two launches, uv
     intermediate in HBM), plus the round-trip error sum (RCCL all-reduce on
@@ -231,6 +250,8 @@ def main():
         config1()
     if "3" in cs:
         config3(int(10_000_000 * a.scale))
+    if "fov" in cs:
+        config_fov(int(10_000_000 * a.scale))
     if "3ne" in cs:
         config3_ne_all(int(10_000_000 * a.scale))
     if "4" in cs:
