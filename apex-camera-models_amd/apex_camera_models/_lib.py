@@ -62,6 +62,7 @@ class LmSummary(ctypes.Structure):
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                 ctypes.c_void_p)
+ERR_NOT_SUPPORTED = -6
 ERR_NUMERICAL = -7
 LM_TERMINATION = {0: "MaxIterations", 1: "CostTolerance", 2: "ParameterTolerance",
                   3: "GradientTolerance", 4: "Failed"}
@@ -96,6 +97,8 @@ EXPORTED_SYMBOLS = (
     "acm_linear_system_qr",
     "acm_linear_estimation_workspace_size",
     "acm_linear_estimation",
+    "acm_linear_system_r_merge",
+    "acm_linear_estimation_solve",
     "acm_fov_grid_workspace_size",
     "acm_fov_grid_errors",
     "acm_fov_grid_select",
@@ -104,6 +107,7 @@ EXPORTED_SYMBOLS = (
     "acm_lm_optimize",
     "acm_median_workspace_size",
     "acm_median_valid",
+    "acm_median_valid_allreduce",
     "acm_sample_points_grid",
     "acm_sample_points_workspace_size",
     "acm_sample_points",
@@ -187,6 +191,11 @@ def load():
     L.acm_linear_estimation_workspace_size.restype = sz
     L.acm_linear_estimation.argtypes = [cam_p, sz, vp, i, vp, vp, sz, vp]
     L.acm_linear_estimation.restype = i
+    L.acm_linear_system_r_merge.argtypes = [i, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_double)]
+    L.acm_linear_system_r_merge.restype = i
+    L.acm_linear_estimation_solve.argtypes = [cam_p, sz, ctypes.POINTER(ctypes.c_double), i]
+    L.acm_linear_estimation_solve.restype = i
     L.acm_fov_grid_workspace_size.argtypes = [sz]
     L.acm_fov_grid_workspace_size.restype = sz
     L.acm_fov_grid_errors.argtypes = [cam_p, sz, vp, i, vp, vp, vp, sz, vp]
@@ -204,6 +213,9 @@ def load():
     L.acm_median_workspace_size.restype = sz
     L.acm_median_valid.argtypes = [sz, vp, vp, ctypes.c_uint64, vp, vp, sz, vp]
     L.acm_median_valid.restype = i
+    L.acm_median_valid_allreduce.argtypes = [sz, vp, vp, ctypes.c_uint64, vp, vp, sz,
+                                             ALLREDUCE_FN, vp, vp]
+    L.acm_median_valid_allreduce.restype = i
     L.acm_undistort_image.argtypes = [cam_p, ctypes.POINTER(ctypes.c_double), i, vp, vp, vp]
     L.acm_undistort_image.restype = i
     L.acm_set_device.argtypes = [i]

@@ -53,14 +53,27 @@ DISPLAY = {"double_sphere": "Double Sphere", "kannala_brandt": "Kannala-Brandt",
 
 
 def convert(input_model: CameraModel, target: str, points_3d, points_2d,
-            config: LevenbergMarquardtConfig = None, allreduce=None) -> ConversionMetrics:
-    """One `convert_to_<target>` (e.g. convert_to_double_sphere :355-488)."""
+            config: LevenbergMarquardtConfig = None, allreduce=None,
+            group=None) -> ConversionMetrics:
+    """One `convert_to_<target>` (e.g. convert_to_double_sphere :355-488).
+
+    Multi-GPU: pass this rank's shard of the correspondences and an
+    `allreduce` hook (distributed.rccl_allreduce(group)); the linear
+    estimation, the LM normal equations and the reprojection statistics then
+    all run over the union of the shards, identically on every rank."""
     import torch
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     model = _init_target(target, input_model)
-    initial = util.compute_reprojection_error(model, points_3d, points_2d)
-    model.linear_estimation(points_3d, points_2d)
+    if allreduce is not None:
+        from . import distributed as D
+        reproj = lambda m: D.distributed_reprojection_error(m, points_3d, points_2d, group)  # noqa: E731
+        estimate = lambda m: D.distributed_linear_estimation(m, points_3d, points_2d, group)  # noqa: E731
+    else:
+        reproj = lambda m: util.compute_reprojection_error(m, points_3d, points_2d)  # noqa: E731
+        estimate = lambda m: m.linear_estimation(points_3d, points_2d)  # noqa: E731
+    initial = reproj(model)
+    estimate(model)
     cfg = config or LevenbergMarquardtConfig()
     status = "Converged"
     res = None
@@ -74,7 +87,7 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
         status = "Linear Only"
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
-    final = util.compute_reprojection_error(model, points_3d, points_2d)
+    final = reproj(model)
     return ConversionMetrics(model=model, model_name=DISPLAY[target],
                              final_reprojection_error=final, initial_reprojection_error=initial,
                              optimization_time_ms=ms, convergence_status=status,

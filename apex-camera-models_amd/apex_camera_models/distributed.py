@@ -75,9 +75,11 @@ def allreduce_normal_equations(vec: torch.Tensor, group=None) -> torch.Tensor:
 
 # --------------------------------------------------- reprojection statistics
 def combine_reprojection_stats(local_errors: torch.Tensor, group=None) -> dict:
-    """error_metrics.rs:86-101 over the union of all ranks' valid errors
+    """error_metrics.rs:86-111 over the union of all ranks' valid errors
     (local_errors: this rank's per-point errors, NaN = failed projection).
-    The median needs a distributed select and is computed by the caller."""
+    Sums / min / max are all-reduced; the median of the union comes from
+    libacm's radix select with its per-pass histograms all-reduced
+    (distributed_median) when the errors live on the GPU."""
     valid = local_errors[~torch.isnan(local_errors)]
     dev = local_errors.device
     s = torch.stack([valid.sum(), (valid * valid).sum(),
@@ -94,8 +96,139 @@ def combine_reprojection_stats(local_errors: torch.Tensor, group=None) -> dict:
     mean = float(s[0]) / n
     var = ((valid - mean) ** 2).sum().reshape(1)
     dist.all_reduce(var, op=dist.ReduceOp.SUM, group=group)
-    return {"rmse": (float(s[1]) / n) ** 0.5, "min": float(mn), "max": float(mx), "mean": mean,
-            "stddev": (float(var) / n) ** 0.5, "n_valid": int(n)}
+    out = {"rmse": (float(s[1]) / n) ** 0.5, "min": float(mn), "max": float(mx), "mean": mean,
+           "stddev": (float(var) / n) ** 0.5, "n_valid": int(n)}
+    if local_errors.is_cuda:
+        out["median"] = distributed_median(local_errors, int(n), group)
+    return out
+
+
+def distributed_median(local_errors: torch.Tensor, n_valid_global: int, group=None) -> float:
+    """Exact median of the union of every rank's non-NaN errors
+    (error_metrics.rs:103-111): acm_median_valid_allreduce, one all-reduce of
+    a 256-bin histogram per radix pass (16 x 2 KB, latency-bound)."""
+    import ctypes
+
+    from . import _lib
+    from .camera import _stream_handle
+    L = _lib.load()
+    e = local_errors.contiguous()
+    out = torch.empty((1,), dtype=torch.float64, device=e.device)
+    ws_bytes = L.acm_median_workspace_size(e.numel())
+    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=e.device)
+    cb = _lib.ALLREDUCE_FN(rccl_allreduce(group))
+    _lib.check(L.acm_median_valid_allreduce(e.numel(), e.data_ptr() if e.numel() else None,
+                                            None, n_valid_global, out.data_ptr(), ws.data_ptr(),
+                                            ws_bytes, cb, None, _stream_handle()))
+    return float(out.item())
+
+
+# ---------------------------------------------------- linear estimation
+def distributed_linear_estimation(model, points_3d, points_2d, group=None) -> None:
+    """`XModel::linear_estimation` over the union of every rank's
+    correspondences.  KB/RadTan/DS/UCM/EUCM: each rank reduces its shard's
+    [A | b] rows to a (k+1)^2 TSQR factor on the GPU, the factors are
+    all-gathered and folded in rank order (acm_linear_system_r_merge), and
+    every rank solves the same system (acm_linear_estimation_solve).  FOV:
+    the all-reduced grid search.  Updates the model in place, identically on
+    every rank."""
+    import ctypes
+
+    from . import _lib
+    from .camera import InvalidParams, NumericalError, _as_device_f64, _stream_handle
+    if model.NAME == "fov":
+        return distributed_fov_linear_estimation(model, points_3d, points_2d, group)
+    L = _lib.load()
+    p3 = _as_device_f64(points_3d, 3)
+    p2 = _as_device_f64(points_2d, 2)
+    if p3.shape[0] != p2.shape[0]:
+        raise InvalidParams("Number of 2D and 3D points must match")
+    n = p3.shape[0]
+    mid = model.MODEL_ID
+    k = L.acm_linear_system_columns(mid)
+    if k < 0:
+        raise InvalidParams(f"{model.NAME} has no linear_estimation")
+    S = (k + 1) * (k + 2) // 2
+    dev = p3.device
+    ws_bytes = L.acm_linear_system_qr_workspace_size(mid, n)
+    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=dev)
+    r_dev = torch.zeros((S + 2,), dtype=torch.float64, device=dev)  # R | err | n
+    err = torch.zeros((1,), dtype=torch.int32, device=dev)
+    cam = model.acm_camera()
+    _lib.check(L.acm_linear_system_qr(ctypes.byref(cam), n, p3.data_ptr() if n else None,
+                                      _lib.LAYOUT_AOS, p2.data_ptr() if n else None,
+                                      r_dev.data_ptr(), err.data_ptr(), ws.data_ptr(), ws_bytes,
+                                      _stream_handle()))
+    r_dev[S] = err[0].to(torch.float64)
+    r_dev[S + 1] = float(n)
+    world = dist.get_world_size(group)
+    parts = [torch.empty_like(r_dev) for _ in range(world)]
+    dist.all_gather(parts, r_dev, group=group)
+    host = [p.cpu().tolist() for p in parts]
+    R = (ctypes.c_double * S)(*host[0][:S])
+    for h in host[1:]:
+        _lib.check(L.acm_linear_system_r_merge(mid, R, (ctypes.c_double * S)(*h[:S])))
+    any_err = int(any(h[S] != 0.0 for h in host))
+    n_total = int(sum(h[S + 1] for h in host))
+    rc = L.acm_linear_estimation_solve(ctypes.byref(cam), n_total, R, any_err)
+    if rc == _lib.ERR_INVALID_PARAMS:
+        raise InvalidParams(_lib.last_error())
+    if rc == _lib.ERR_NUMERICAL:
+        raise NumericalError(_lib.last_error())
+    _lib.check(rc)
+    model._set_params(list(cam.params)[: model.NUM_PARAMS])
+
+
+def distributed_reprojection_error(model, points_3d, points_2d, group=None):
+    """`compute_reprojection_error` (error_metrics.rs:62-121) over the union of
+    every rank's correspondences (GPU per-point errors, all-reduced sums and
+    extrema, distributed exact median)."""
+    from . import util
+    from .camera import _as_device_f64
+    p3 = _as_device_f64(points_3d, 3)
+    errors = torch.empty((p3.shape[0],), dtype=torch.float64, device=p3.device)
+    util.reprojection_stats(model, p3, points_2d, errors)
+    st = combine_reprojection_stats(errors, group)
+    if st["n_valid"] == 0:
+        raise util.ZeroProjectionPoints()
+    return util.ProjectionError(rmse=st["rmse"], min=st["min"], max=st["max"], mean=st["mean"],
+                                stddev=st["stddev"], median=st["median"], n_valid=st["n_valid"])
+
+
+# ------------------------------------------------------ FOV grid search
+def distributed_fov_linear_estimation(model, points_3d, points_2d, group=None) -> None:
+    """FovModel::linear_estimation (fov.rs:153-251) over the union of every
+    rank's correspondences: each rank runs the 290-value grid on its shard
+    (acm_fov_grid_errors), the 2 x 290 sums are all-reduced, and every rank
+    selects the same w (acm_fov_grid_select).  Updates model.w in place."""
+    import ctypes
+
+    from . import _lib
+    from .camera import InvalidParams, _as_device_f64, _stream_handle
+    L = _lib.load()
+    p3 = _as_device_f64(points_3d, 3)
+    p2 = _as_device_f64(points_2d, 2)
+    if p3.shape[0] != p2.shape[0]:
+        raise InvalidParams("Number of 2D and 3D points must match")
+    n = p3.shape[0]
+    total = torch.tensor([float(n)], dtype=torch.float64, device=p3.device)
+    dist.all_reduce(total, op=dist.ReduceOp.SUM, group=group)
+    if float(total) < 2:  # fov.rs:166-171
+        raise InvalidParams("Need at least 2 point correspondences for linear estimation")
+    ws_bytes = L.acm_fov_grid_workspace_size(n)
+    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=p3.device)
+    sums = torch.empty((2 * _lib.FOV_GRID_SIZE,), dtype=torch.float64, device=p3.device)
+    cam = model.acm_camera()
+    _lib.check(L.acm_fov_grid_errors(ctypes.byref(cam), n, p3.data_ptr() if n else None,
+                                     _lib.LAYOUT_AOS, p2.data_ptr() if n else None,
+                                     sums.data_ptr(), ws.data_ptr(), ws_bytes, _stream_handle()))
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+    host = (ctypes.c_double * (2 * _lib.FOV_GRID_SIZE))(*sums.cpu().tolist())
+    rc = L.acm_fov_grid_select(ctypes.byref(cam), host)
+    if rc == _lib.ERR_INVALID_PARAMS:
+        raise InvalidParams(_lib.last_error())
+    _lib.check(rc)
+    model._set_params(list(cam.params)[: model.NUM_PARAMS])
 
 
 # ------------------------------------------------------------ sample_points

@@ -700,9 +700,12 @@ struct SelState {
     unsigned long long prefix, mask, k;
 };
 
+// Histogram counts are kept as f64 (exact below 2^53, and integer sums are
+// order-independent) so a multi-GPU caller can all-reduce them in place with
+// the same f64 callback the LM uses.
 __global__ __launch_bounds__(kBlock) void k_sel_hist(size_t n, const double* __restrict__ vals,
                                                      const SelState* __restrict__ st, int shift,
-                                                     unsigned long long* __restrict__ hist) {
+                                                     double* __restrict__ hist) {
     __shared__ unsigned int h[256];
     h[threadIdx.x] = 0;  // kBlock == 256
     __syncthreads();
@@ -713,28 +716,28 @@ __global__ __launch_bounds__(kBlock) void k_sel_hist(size_t n, const double* __r
         if ((b & mask) == prefix) atomicAdd(&h[(b >> shift) & 0xFFull], 1u);
     }
     __syncthreads();
-    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (double)h[threadIdx.x]);
 }
 
-__global__ void k_sel_pick(SelState* __restrict__ st, int shift,
-                           unsigned long long* __restrict__ hist) {
+__global__ void k_sel_pick(SelState* __restrict__ st, int shift, double* __restrict__ hist) {
     if (threadIdx.x != 0) return;
     unsigned long long k = st->k, run = 0;
     int b = 0;
     for (; b < 256; ++b) {
-        if (run + hist[b] > k) break;
-        run += hist[b];
+        const unsigned long long c = (unsigned long long)hist[b];
+        if (run + c > k) break;
+        run += c;
     }
     if (b == 256) b = 255;
     st->k = k - run;
     st->prefix |= (unsigned long long)b << shift;
     st->mask |= 0xFFull << shift;
-    for (int j = 0; j < 256; ++j) hist[j] = 0;
+    for (int j = 0; j < 256; ++j) hist[j] = 0.0;
 }
 
 __global__ void k_sel_init(SelState* __restrict__ st, const double* __restrict__ nvalid_src,
                            unsigned long long nvalid_fixed, int which,
-                           unsigned long long* __restrict__ hist) {
+                           double* __restrict__ hist) {
     if (threadIdx.x != 0) return;
     const unsigned long long m =
         nvalid_src ? (unsigned long long)nvalid_src[0] : nvalid_fixed;
@@ -742,7 +745,7 @@ __global__ void k_sel_init(SelState* __restrict__ st, const double* __restrict__
     st->k = which == 0 ? (m ? (m - 1) / 2 : 0) : m / 2;
     st->prefix = 0;
     st->mask = 0;
-    for (int j = 0; j < 256; ++j) hist[j] = 0;
+    for (int j = 0; j < 256; ++j) hist[j] = 0.0;
 }
 
 __global__ void k_sel_finish(const SelState* __restrict__ a, const SelState* __restrict__ b,
@@ -1611,19 +1614,21 @@ ACM_API int acm_fov_grid_errors(const acm_camera* cam, size_t n, const double* p
 
 ACM_API size_t acm_median_workspace_size(size_t n) {
     (void)n;
-    return 2 * sizeof(SelState) + 256 * sizeof(unsigned long long);
+    return 2 * sizeof(SelState) + 256 * sizeof(double);
 }
 
-ACM_API int acm_median_valid(size_t n, const double* values, const double* n_valid_device,
-                             uint64_t n_valid, double* out, void* workspace,
-                             size_t workspace_bytes, void* stream) {
+ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
+                                       const double* n_valid_device, uint64_t n_valid,
+                                       double* out, void* workspace, size_t workspace_bytes,
+                                       acm_allreduce_fn allreduce, void* allreduce_ctx,
+                                       void* stream) {
     if (!out || !workspace || (n && !values)) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
     if (workspace_bytes < acm_median_workspace_size(n))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "median workspace too small");
     hipStream_t s = (hipStream_t)stream;
     SelState* sa = (SelState*)workspace;
     SelState* sb = sa + 1;
-    unsigned long long* hist = (unsigned long long*)(sb + 1);
+    double* hist = (double*)(sb + 1);
     const unsigned nb = (unsigned)ne_blocks(n);
     for (int which = 0; which < 2; ++which) {
         SelState* st = which ? sb : sa;
@@ -1632,12 +1637,25 @@ ACM_API int acm_median_valid(size_t n, const double* values, const double* n_val
         for (int shift = 56; shift >= 0; shift -= 8) {
             hipLaunchKernelGGL(k_sel_hist, dim3(nb), dim3(kBlock), 0, s, n, values, st, shift,
                                hist);
+            if (allreduce) {  // every rank then picks the same digit
+                int rc = check_launch("acm_median_valid (histogram)");
+                if (rc) return rc;
+                if (allreduce(allreduce_ctx, hist, 256, stream) != 0)
+                    return fail(ACM_ERR_INVALID_ARGUMENT, "allreduce callback failed");
+            }
             hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(64), 0, s, st, shift, hist);
         }
     }
     hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(64), 0, s, sa, sb, n_valid_device,
                        (unsigned long long)n_valid, out);
     return check_launch("acm_median_valid");
+}
+
+ACM_API int acm_median_valid(size_t n, const double* values, const double* n_valid_device,
+                             uint64_t n_valid, double* out, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+    return acm_median_valid_allreduce(n, values, n_valid_device, n_valid, out, workspace,
+                                      workspace_bytes, nullptr, nullptr, stream);
 }
 
 

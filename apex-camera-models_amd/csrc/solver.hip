@@ -165,38 +165,60 @@ ACM_API size_t acm_linear_estimation_workspace_size(int model, size_t n) {
 
 // linear_estimation (kannala_brandt.rs:164-272, double_sphere.rs:225-290,
 // ucm.rs:200-258, eucm.rs:216-288, rad_tan.rs:153-234): updates cam->params.
-ACM_API int acm_linear_estimation(acm_camera* cam, size_t n, const double* points_3d, int layout,
-                                  const double* points_2d, void* workspace,
-                                  size_t workspace_bytes, void* stream) {
-    if (!cam) return sfail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
-    if (cam->model == ACM_FOV) return fov_linear_estimation(cam, n, points_3d, layout, points_2d,
-                                                            workspace, workspace_bytes, stream);
+static int count_check(int model, size_t n) {
+    if (model == ACM_KANNALA_BRANDT && n < 4)  // kannala_brandt.rs:174-178
+        return sfail(ACM_ERR_INVALID_PARAMS, "Not enough points for linear estimation (need at least 4)");
+    if (model == ACM_RADTAN && n < 3)  // rad_tan.rs:152-156
+        return sfail(ACM_ERR_INVALID_PARAMS, "Need at least 3 points for RadTan linear estimation");
+    if (model == ACM_EUCM && n < 1)  // eucm.rs:228-232
+        return sfail(ACM_ERR_INVALID_PARAMS, "Need at least 1 point for EUCM linear estimation");
+    return ACM_SUCCESS;
+}
+
+// Givens fold of one packed upper-triangular (M x M) factor into another:
+// the host twin of tri_merge in acm.hip.  qr([R_a; R_b]) = R of the
+// stacked rows of both shards, so a multi-GPU caller merges the per-rank
+// factors in rank order and every rank gets the same R.
+ACM_API int acm_linear_system_r_merge(int model, double* r_inout, const double* r_other) {
+    const int k = acm_linear_system_columns(model);
+    if (k < 0) return sfail(ACM_ERR_NOT_SUPPORTED, "model has no linear_estimation");
+    if (!r_inout || !r_other) return sfail(ACM_ERR_INVALID_ARGUMENT, "NULL factor");
+    const int M = k + 1;
+    auto at = [M](int r, int c) { return r * M - r * (r - 1) / 2 + (c - r); };
+    for (int r0 = 0; r0 < M; ++r0) {
+        double row[8];
+        for (int c = 0; c < M; ++c) row[c] = c < r0 ? 0.0 : r_other[at(r0, c)];
+        for (int j = 0; j < M; ++j) {
+            const double b = row[j];
+            if (b == 0.0) continue;
+            const double a = r_inout[at(j, j)];
+            const double r = std::sqrt(a * a + b * b);
+            const double c = a / r, sn = b / r;
+            r_inout[at(j, j)] = r;
+            for (int l = j + 1; l < M; ++l) {
+                const double Rl = r_inout[at(j, l)], rl = row[l];
+                r_inout[at(j, l)] = c * Rl + sn * rl;
+                row[l] = c * rl - sn * Rl;
+            }
+        }
+    }
+    return ACM_SUCCESS;
+}
+
+// The host half of linear_estimation: solve R_A x = z from the (k+1) x (k+1)
+// factor of [A | b] with nalgebra's SVD::solve(eps) semantics, apply the
+// model's clamps and validation (n_total: the global point count, for the
+// reference's minimum-count checks).
+ACM_API int acm_linear_estimation_solve(acm_camera* cam, size_t n_total,
+                                        const double* r_factor_host, int error_flag) {
+    if (!cam || !r_factor_host) return sfail(ACM_ERR_INVALID_ARGUMENT, "NULL argument");
     const int k = acm_linear_system_columns(cam->model);
     if (k < 0) return sfail(ACM_ERR_NOT_SUPPORTED, "model has no linear_estimation");
-    if (cam->model == ACM_KANNALA_BRANDT && n < 4)  // :174-178
-        return sfail(ACM_ERR_INVALID_PARAMS, "Not enough points for linear estimation (need at least 4)");
-    if (cam->model == ACM_RADTAN && n < 3)  // rad_tan.rs:152-156
-        return sfail(ACM_ERR_INVALID_PARAMS, "Need at least 3 points for RadTan linear estimation");
-    if (cam->model == ACM_EUCM && n < 1)  // eucm.rs:228-232
-        return sfail(ACM_ERR_INVALID_PARAMS, "Need at least 1 point for EUCM linear estimation");
-    const size_t need = acm_linear_estimation_workspace_size(cam->model, n);
-    if (!workspace || workspace_bytes < need)
-        return sfail(ACM_ERR_WORKSPACE_TOO_SMALL, "linear-estimation workspace too small");
-    const int M = k + 1, S = M * (M + 1) / 2;
-    const size_t qr = acm_linear_system_qr_workspace_size(cam->model, n);
-    double* d_r = (double*)((char*)workspace + qr);
-    int* d_err = (int*)(d_r + 16);
-    int rc = acm_linear_system_qr(cam, n, points_3d, layout, points_2d, d_r, d_err, workspace, qr,
-                                  stream);
+    int rc = count_check(cam->model, n_total);
     if (rc) return rc;
-    double R[16];
-    int err = 0;
-    hipStream_t s = (hipStream_t)stream;
-    if (hip_ok(hipMemcpyAsync(R, d_r, S * sizeof(double), hipMemcpyDeviceToHost, s)) ||
-        hip_ok(hipMemcpyAsync(&err, d_err, sizeof(int), hipMemcpyDeviceToHost, s)) ||
-        hip_ok(hipStreamSynchronize(s)))
-        return sfail(ACM_ERR_HIP, "linear estimation: device copy failed");
-    if (err) return sfail(ACM_ERR_NUMERICAL, "fx * x_r is zero in linear estimation");
+    if (error_flag) return sfail(ACM_ERR_NUMERICAL, "fx * x_r is zero in linear estimation");
+    const int M = k + 1;
+    const double* R = r_factor_host;
     // R = [[R_A, z], [0, rho]] (packed upper triangle, row-major)
     double RA[16] = {0}, z[4] = {0}, x[4] = {0};
     auto at = [M](int r, int c) { return r * M - r * (r - 1) / 2 + (c - r); };
@@ -236,6 +258,36 @@ ACM_API int acm_linear_estimation(acm_camera* cam, size_t n, const double* point
         return ACM_SUCCESS;
     default: return sfail(ACM_ERR_NOT_SUPPORTED, "unsupported model");
     }
+}
+
+ACM_API int acm_linear_estimation(acm_camera* cam, size_t n, const double* points_3d, int layout,
+                                  const double* points_2d, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+    if (!cam) return sfail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
+    if (cam->model == ACM_FOV) return fov_linear_estimation(cam, n, points_3d, layout, points_2d,
+                                                            workspace, workspace_bytes, stream);
+    const int k = acm_linear_system_columns(cam->model);
+    if (k < 0) return sfail(ACM_ERR_NOT_SUPPORTED, "model has no linear_estimation");
+    int rc = count_check(cam->model, n);
+    if (rc) return rc;
+    const size_t need = acm_linear_estimation_workspace_size(cam->model, n);
+    if (!workspace || workspace_bytes < need)
+        return sfail(ACM_ERR_WORKSPACE_TOO_SMALL, "linear-estimation workspace too small");
+    const int M = k + 1, S = M * (M + 1) / 2;
+    const size_t qr = acm_linear_system_qr_workspace_size(cam->model, n);
+    double* d_r = (double*)((char*)workspace + qr);
+    int* d_err = (int*)(d_r + 16);
+    rc = acm_linear_system_qr(cam, n, points_3d, layout, points_2d, d_r, d_err, workspace, qr,
+                              stream);
+    if (rc) return rc;
+    double R[16];
+    int err = 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (hip_ok(hipMemcpyAsync(R, d_r, S * sizeof(double), hipMemcpyDeviceToHost, s)) ||
+        hip_ok(hipMemcpyAsync(&err, d_err, sizeof(int), hipMemcpyDeviceToHost, s)) ||
+        hip_ok(hipStreamSynchronize(s)))
+        return sfail(ACM_ERR_HIP, "linear estimation: device copy failed");
+    return acm_linear_estimation_solve(cam, n, R, err);
 }
 
 ACM_API void acm_lm_default_config(acm_lm_config* cfg) {

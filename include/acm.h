@@ -201,6 +201,16 @@ ACM_API int acm_linear_system_qr(const acm_camera *cam, size_t n,
                                  int *error_flag, void *workspace,
                                  size_t workspace_bytes, void *stream);
 ACM_API size_t acm_linear_estimation_workspace_size(int model, size_t n);
+/* Multi-GPU linear_estimation: each rank runs acm_linear_system_qr on its
+ * shard, the packed factors (host copies) are folded in rank order with
+ * acm_linear_system_r_merge (Givens; R of the stacked rows), error flags
+ * OR-ed, and acm_linear_estimation_solve finishes on every rank with the
+ * global point count.  acm_linear_estimation = qr + solve on one GPU. */
+ACM_API int acm_linear_system_r_merge(int model, double *r_inout,
+                                      const double *r_other);
+ACM_API int acm_linear_estimation_solve(acm_camera *cam, size_t n_total,
+                                        const double *r_factor_host,
+                                        int error_flag);
 ACM_API int acm_linear_estimation(acm_camera *cam, size_t n,
                                   const double *points_3d, int layout,
                                   const double *points_2d, void *workspace,
@@ -278,12 +288,23 @@ ACM_API int acm_lm_optimize(acm_camera *cam, size_t n, const double *points_3d,
  * m/2-1 and m/2 for even m, rank m/2 for odd m, m = n_valid (read from
  * device memory n_valid_device if non-NULL, e.g. result[5] of
  * acm_reprojection_stats, else the host value n_valid).  Values must be
- * >= 0 or NaN.  out: device f64. */
+ * >= 0 or NaN.  out: device f64.
+ * acm_median_valid_allreduce is the multi-GPU form: `values` is this
+ * rank's shard, n_valid the GLOBAL count, and after each of the 16
+ * histogram passes the 256-bin f64 histogram (device) goes through the
+ * allreduce callback (a sum over ranks), so every rank selects the same
+ * digits and returns the median of the union. */
 ACM_API size_t acm_median_workspace_size(size_t n);
 ACM_API int acm_median_valid(size_t n, const double *values,
                              const double *n_valid_device, uint64_t n_valid,
                              double *out, void *workspace,
                              size_t workspace_bytes, void *stream);
+ACM_API int acm_median_valid_allreduce(size_t n, const double *values,
+                                       const double *n_valid_device,
+                                       uint64_t n_valid, double *out,
+                                       void *workspace, size_t workspace_bytes,
+                                       acm_allreduce_fn allreduce,
+                                       void *allreduce_ctx, void *stream);
 
 /* util::sample_points (point_sampling.rs:46-120): a grid of
  * round(sqrt(n*w/h)) x round(sqrt(n*h/w)) cell centres (row-major, as the

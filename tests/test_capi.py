@@ -134,3 +134,37 @@ def test_newton_tolerance_threshold_is_exact():
         s = np.nextafter(s, np.inf)
     for v in (0.0, 1e-300, 1e-13, 1e-12, 1.0, math.inf):
         assert (math.sqrt(v) < 1e-6) == (v < t)
+
+
+def _packed_r(A):
+    import numpy as np
+    R = np.linalg.qr(A, mode="r")
+    R = R * np.sign(np.where(np.diag(R) == 0, 1.0, np.diag(R)))[:, None]
+    M = R.shape[0]
+    return np.array([R[r, c] for r in range(M) for c in range(r, M)])
+
+
+@pytest.mark.parametrize("model,k", [(2, 4), (1, 3), (3, 1)])
+def test_linear_system_r_merge_is_qr_of_stacked_rows(model, k):
+    # the multi-GPU linear_estimation fold: merge(R(A1), R(A2)) = R([A1; A2])
+    import numpy as np
+    from apex_camera_models import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(k)
+    A1, A2 = rng.normal(size=(50, k + 1)), rng.normal(size=(37, k + 1))
+    r1, r2 = _packed_r(A1), _packed_r(A2)
+    a = (ctypes.c_double * len(r1))(*r1)
+    b = (ctypes.c_double * len(r2))(*r2)
+    assert L.acm_linear_system_r_merge(model, a, b) == 0
+    np.testing.assert_allclose(np.array(a[:]), _packed_r(np.vstack([A1, A2])), rtol=1e-12,
+                               atol=1e-12)
+    assert L.acm_linear_system_r_merge(6, a, b) == _lib.ERR_NOT_SUPPORTED
+
+
+def test_linear_estimation_solve_host_checks():
+    from apex_camera_models import _lib
+    L = _lib.load()
+    _, cam = _init(2, [190.0, 190.0, 254.0, 256.0, 0.0, 0.0, 0.0, 0.0], 512, 512)
+    r = (ctypes.c_double * 15)(*([0.0] * 15))
+    assert L.acm_linear_estimation_solve(ctypes.byref(cam), 3, r, 0) == _lib.ERR_INVALID_PARAMS
+    assert L.acm_linear_estimation_solve(ctypes.byref(cam), 10, r, 1) == _lib.ERR_NUMERICAL
