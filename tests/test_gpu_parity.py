@@ -267,3 +267,47 @@ def test_f32_path_tracks_f64(golden_dir, model):
     u0 = g["uv"][keep][both]
     err = np.abs(uv.cpu().numpy()[both].astype(np.float64) - u0) / np.maximum(np.abs(u0), 1.0)
     assert np.nanmax(err) < 1e-4
+
+
+@pytest.mark.parametrize("model", [2, 3])
+def test_buffers_at_8_byte_offsets(golden_dir, model):
+    """The C-ABI takes plain f64 pointers: a caller may hand sub-views that are
+    only 8-byte aligned (e.g. a Matrix2xX slice starting at an odd column
+    offset of a larger buffer).  Every 16-B vector store must still land
+    correctly -- same results as 16-B-aligned buffers."""
+    import ctypes
+
+    import torch
+    from apex_camera_models import _lib
+    g = np.load(os.path.join(golden_dir, f"golden_{model}.npz"))
+    params = g["params"].tolist()
+    w, h = int(g["res"][0]), int(g["res"][1])
+    pts = g["xyz"]
+    n = len(pts)
+    P = len(params)
+    L = _lib.load()
+    m = GpuBackend()._model(model, params, w, h)
+    cam = m.acm_camera()
+    base_p = torch.zeros(3 * n + 1, dtype=torch.float64, device="cuda")
+    base_p[1:] = torch.as_tensor(pts.ravel(), device="cuda")
+    uv = torch.full((2 * n + 1,), 7.0, dtype=torch.float64, device="cuda")
+    st = torch.zeros(n + 1, dtype=torch.uint8, device="cuda")
+    jac = torch.full((2 * n * P + 1,), 7.0, dtype=torch.float64, device="cuda")
+    _lib.check(L.acm_project(ctypes.byref(cam), n, base_p.data_ptr() + 8, 0, uv.data_ptr() + 8,
+                             st.data_ptr() + 1, jac.data_ptr() + 8, None))
+    nu = len(g["uv_in"])
+    uvin = torch.zeros(2 * nu + 1, dtype=torch.float64, device="cuda")
+    uvin[1:] = torch.as_tensor(g["uv_in"].ravel(), device="cuda")
+    rays = torch.full((3 * nu + 1,), 7.0, dtype=torch.float64, device="cuda")
+    st2 = torch.zeros(nu + 1, dtype=torch.uint8, device="cuda")
+    _lib.check(L.acm_unproject(ctypes.byref(cam), nu, uvin.data_ptr() + 8, rays.data_ptr() + 8,
+                               0, st2.data_ptr() + 1, None))
+    torch.cuda.synchronize()
+    ref_uv, ref_st, ref_j = GpuBackend().project(model, params, w, h, pts)
+    assert uv[0].item() == 7.0 and jac[0].item() == 7.0  # nothing written before the view
+    assert np.array_equal(st[1:].cpu().numpy(), ref_st)
+    assert np.array_equal(uv[1:].cpu().numpy().reshape(n, 2), ref_uv, equal_nan=True)
+    assert np.array_equal(jac[1:].cpu().numpy().reshape(P, n, 2), ref_j, equal_nan=True)
+    ref_r, ref_s2 = GpuBackend().unproject(model, params, w, h, g["uv_in"])
+    assert np.array_equal(st2[1:].cpu().numpy(), ref_s2)
+    assert np.array_equal(rays[1:].cpu().numpy().reshape(nu, 3), ref_r, equal_nan=True)
