@@ -125,6 +125,8 @@ static int g_project_variant = -1;
 // measured slower here (DS, 9.3M points: 0.273 ms plain vs 0.310 ms nt,
 // profiles/r01_configs.log); -1 = auto (nt above kNtThresholdBytes), 1 = on.
 static int g_residual_nt = 0;
+// Normal equations: minimum waves per SIMD for the register allocator (1, 3, 4).
+static int g_ne_waves = 3;
 constexpr size_t kNtThresholdBytes = 256ull << 20;
 
 template <class TagT, int LAYOUT, bool WJ, bool NT>
@@ -364,8 +366,12 @@ static int nq_blocks(size_t n) {
     return (int)b;
 }
 
-template <class TagT, int LAYOUT>
-__global__ __launch_bounds__(kBlock) void k_normal_eq(acm_camera cam, size_t n,
+// WAVES: minimum waves per SIMD the register allocator must allow
+// (amdgpu_waves_per_eu).  1 leaves it free (KB lands at 176 VGPRs = 2 waves);
+// 3 fits KB in 168 without spills; 4 forces 128 with scratch spills for KB and
+// RadTan.  Selected per launch by ACM_TUNE_NE_WAVES (results identical).
+template <class TagT, int LAYOUT, int WAVES>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq(acm_camera cam, size_t n,
                                                       const double* __restrict__ pts,
                                                       const double* __restrict__ obs, int policy,
                                                       double* __restrict__ parts) {
@@ -382,10 +388,13 @@ __global__ __launch_bounds__(kBlock) void k_normal_eq(acm_camera cam, size_t n,
     const size_t stride = (size_t)gridDim.x * kBlock;
     size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
     // software pipeline: the next point's 40 bytes are in flight while the
-    // current one is projected and accumulated
+    // current one is projected and accumulated.  Not for the largest
+    // accumulator sets (KB, RadTan), where the extra 10 VGPRs cost a wave of
+    // occupancy.
+    constexpr bool kPrefetch = K <= 40;
     double x = 0, y = 0, z = 1;
     double2 o = make_double2(0.0, 0.0);
-    if (i < n) {
+    if (kPrefetch && i < n) {
         load_point<LAYOUT>(pts, n, i, x, y, z);
         o = *reinterpret_cast<const double2*>(obs + 2 * i);
     }
@@ -393,9 +402,14 @@ __global__ __launch_bounds__(kBlock) void k_normal_eq(acm_camera cam, size_t n,
         const size_t inext = i + stride;
         double xn = 0, yn = 0, zn = 1;
         double2 on = make_double2(0.0, 0.0);
-        if (inext < n) {
-            load_point<LAYOUT>(pts, n, inext, xn, yn, zn);
-            on = *reinterpret_cast<const double2*>(obs + 2 * inext);
+        if (kPrefetch) {
+            if (inext < n) {
+                load_point<LAYOUT>(pts, n, inext, xn, yn, zn);
+                on = *reinterpret_cast<const double2*>(obs + 2 * inext);
+            }
+        } else {
+            load_point<LAYOUT>(pts, n, i, x, y, z);
+            o = *reinterpret_cast<const double2*>(obs + 2 * i);
         }
         double u, v, ju[P], jv[P];
         const uint8_t st = M::template project<true>(c, x, y, z, u, v, ju, jv);
@@ -430,7 +444,7 @@ __global__ __launch_bounds__(kBlock) void k_normal_eq(acm_camera cam, size_t n,
         } else {
             acc[K - 2] += sent2;
         }
-        x = xn; y = yn; z = zn; o = on;
+        if (kPrefetch) { x = xn; y = yn; z = zn; o = on; }
     }
     block_sum_store<K>(acc, parts + (size_t)blockIdx.x * K);
 }
@@ -1371,12 +1385,20 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
         constexpr int K = NE<P>::K;
         double* parts = (double*)workspace;
         double* sums = parts + (size_t)nb * K;
-        if (layout == ACM_LAYOUT_AOS)
-            hipLaunchKernelGGL((k_normal_eq<TagT, ACM_LAYOUT_AOS>), dim3(nb), dim3(kBlock), 0, s,
-                               prep(*cam), n, points_3d, points_2d_obs, invalid_policy, parts);
-        else
-            hipLaunchKernelGGL((k_normal_eq<TagT, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s,
-                               prep(*cam), n, points_3d, points_2d_obs, invalid_policy, parts);
+        auto go = [&](auto lay_c, auto w_c) {
+            hipLaunchKernelGGL((k_normal_eq<TagT, decltype(lay_c)::value, decltype(w_c)::value>),
+                               dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
+                               points_2d_obs, invalid_policy, parts);
+        };
+        auto by_waves = [&](auto lay_c) {
+            switch (g_ne_waves) {
+            case 1: go(lay_c, std::integral_constant<int, 1>{}); break;
+            case 4: go(lay_c, std::integral_constant<int, 4>{}); break;
+            default: go(lay_c, std::integral_constant<int, 3>{}); break;
+            }
+        };
+        if (layout == ACM_LAYOUT_AOS) by_waves(std::integral_constant<int, ACM_LAYOUT_AOS>{});
+        else by_waves(std::integral_constant<int, ACM_LAYOUT_SOA>{});
         hipLaunchKernelGGL(k_sum_columns, dim3(K), dim3(kBlock), 0, s, parts, nb, K, sums);
         hipLaunchKernelGGL(k_ne_expand<P>, dim3(1), dim3(64), 0, s, sums, result);
         return check_launch("acm_normal_equations");
@@ -1724,6 +1746,13 @@ ACM_API int acm_set_tuning(int key, int value) {
         if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
         const int old = g_residual_nt;
         g_residual_nt = value;
+        return old;
+    }
+    if (key == ACM_TUNE_NE_WAVES) {
+        if (value != 1 && value != 3 && value != 4)
+            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 1, 3 or 4");
+        const int old = g_ne_waves;
+        g_ne_waves = value;
         return old;
     }
     return fail(ACM_ERR_INVALID_ARGUMENT, "unknown tuning key");

@@ -357,9 +357,10 @@ ACM_API int acm_stream_synchronize(void *stream);
  * kernel, 1 = non-temporal stores, 2 = persistent grid-stride launch,
  * 4 = two points per lane; -1 (default) = auto (non-temporal stores when the
  * outputs exceed 256 MiB).  ACM_TUNE_RESIDUAL_NT: non-temporal stores in
- * acm_residual_jacobian (-1 auto, 0 off = default, 1 on).  Returns the previous value
- * or an error. */
-enum { ACM_TUNE_PROJECT_VARIANT = 0, ACM_TUNE_RESIDUAL_NT = 1 };
+ * acm_residual_jacobian (-1 auto, 0 off = default, 1 on).  ACM_TUNE_NE_WAVES:
+ * minimum waves per SIMD the normal-equations kernel is compiled for
+ * (1, 3 = default, 4).  Returns the previous value or an error. */
+enum { ACM_TUNE_PROJECT_VARIANT = 0, ACM_TUNE_RESIDUAL_NT = 1, ACM_TUNE_NE_WAVES = 2 };
 ACM_API int acm_set_tuning(int key, int value);
 
 /* Diagnostics: last HIP error code / message of the calling thread. */

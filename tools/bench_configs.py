@@ -116,8 +116,8 @@ def config3(n_target):
 def config3_ne_all(n):
     """Fused normal equations for every model on the same synthetic batch."""
     import torch
-    from apex_camera_models import factors, samples
-    from apex_camera_models.camera import MODEL_CLASSES, Resolution
+    from apex_camera_models import _lib, factors, samples
+    from apex_camera_models.camera import Resolution
     pts = samples.synthetic_points_device(n)
     pts = pts[torch.isfinite(pts).all(1)].contiguous()
     n = pts.shape[0]
@@ -133,10 +133,23 @@ def config3_ne_all(n):
         f = fcls(pts, obs, Resolution(w, h))
         P = len(params)
         out = torch.empty((P * P + P + 2,), dtype=torch.float64, device="cuda")
-        ms = timed(lambda: f.normal_equations(params, out))
+        L = _lib.load()
+        res = {}
+        for rep in range(2):  # interleaved A/B of the register-allocation target
+            for wv in (1, 3, 4):
+                L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)
+                res.setdefault(wv, []).append(timed(lambda: f.normal_equations(params, out)))
+                if rep == 0 and wv == 1:
+                    ref = out.clone()
+                elif rep == 0:
+                    assert torch.equal(out, ref), "NE result depends on the waves target"
+        L.acm_set_tuning(_lib.TUNE_NE_WAVES, 3)
+        ms = {wv: min(v) for wv, v in res.items()}
+        best = min(ms, key=ms.get)
         emit({"config": 3, "what": "fused normal equations", "model": fcls.MODEL.__name__,
-              "points": n, "ms": round(ms, 4), "Mpoints_per_s": round(n / ms / 1e3, 1),
-              "GBps": round(40 * n / ms / 1e6, 1)})
+              "points": n, "ms_by_waves": {str(k): round(v, 4) for k, v in ms.items()},
+              "best_waves": best, "Mpoints_per_s": round(n / ms[best] / 1e3, 1),
+              "GBps": round(40 * n / ms[best] / 1e6, 1)})
 
 
 def config_fov(n_target):
