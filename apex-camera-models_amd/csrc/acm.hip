@@ -19,7 +19,10 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <type_traits>
 
@@ -349,7 +352,7 @@ struct NE {
     static constexpr int K = G + 4 + D + 2;
 };
 
-constexpr int kNeMaxBlocks = 1024;  // reprojection stats / median partials
+constexpr int kNeMaxBlocks = 2048;  // reprojection stats / median partials
 constexpr int kNqMaxBlocks = 2048;  // normal equations: 8 workgroups per CU
 
 static int ne_blocks(size_t n) {
@@ -364,6 +367,32 @@ static int nq_blocks(size_t n) {
     if (b > (size_t)kNqMaxBlocks) b = kNqMaxBlocks;
     if (b == 0) b = 1;
     return (int)b;
+}
+
+// Workgroups of `kernel` (kBlock lanes) that are resident on the whole
+// device at once: occupancy per CU x CU count, cached per (kernel, device).
+// Grid-stride reductions launch at most this many, so every workgroup starts
+// in the first wave of dispatch -- a grid larger than the resident capacity
+// leaves a second, partial round running alone at the end (a 2048-block
+// launch of a 7-waves/SIMD kernel is 1.14 rounds).
+static int resident_blocks(const void* kernel) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return kNqMaxBlocks;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find({kernel, dev});
+    if (it != cache.end()) return it->second;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        per_cu <= 0 || cus <= 0) {
+        (void)hipGetLastError();
+        return kNqMaxBlocks;
+    }
+    const int r = per_cu * cus;
+    cache[{kernel, dev}] = r;
+    return r;
 }
 
 // WAVES: minimum waves per SIMD the register allocator must allow
@@ -883,7 +912,7 @@ struct LinRows<ACM_RADTAN> {  // rad_tan.rs:168-198, k = 3
     }
 };
 
-constexpr int kTsqrMaxBlocks = 1024;
+constexpr int kTsqrMaxBlocks = 2048;
 
 template <int MODEL, int LAYOUT>
 __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
@@ -1377,17 +1406,20 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
     if (workspace_bytes < acm_normal_equations_workspace_size(cam->model, n))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "normal-equations workspace too small");
     hipStream_t s = (hipStream_t)stream;
-    const int nb = nq_blocks(n);
+    const int nb_max = nq_blocks(n);
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
         using M = typename TagT::template type<double>;
         constexpr int P = M::P;
         constexpr int K = NE<P>::K;
         double* parts = (double*)workspace;
-        double* sums = parts + (size_t)nb * K;
+        double* sums = parts + (size_t)nb_max * K;
+        int nb = nb_max;
         auto go = [&](auto lay_c, auto w_c) {
-            hipLaunchKernelGGL((k_normal_eq<TagT, decltype(lay_c)::value, decltype(w_c)::value>),
-                               dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
+            auto kern = k_normal_eq<TagT, decltype(lay_c)::value, decltype(w_c)::value>;
+            const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
+            if (nb > cap) nb = cap;
+            hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
                                points_2d_obs, invalid_policy, parts);
         };
         auto by_waves = [&](auto lay_c) {
@@ -1423,24 +1455,28 @@ ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double
     if (workspace_bytes < acm_reprojection_stats_workspace_size(n))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "reprojection-stats workspace too small");
     hipStream_t s = (hipStream_t)stream;
-    const int nb = ne_blocks(n);
+    const int nb_max = ne_blocks(n);
     double* ws = (double*)workspace;
     double* errs = errors ? errors : ws;
     double* p1 = ws + n;
-    double* tot = p1 + (size_t)nb * 5;
+    double* tot = p1 + (size_t)nb_max * 5;
     double* p2 = tot + 5;
-    double* var = p2 + nb;
+    double* var = p2 + nb_max;
+    const int nb2 = std::min(nb_max, resident_blocks(reinterpret_cast<const void*>(k_reproj_pass2)));
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
-        if (layout == ACM_LAYOUT_AOS)
-            hipLaunchKernelGGL((k_reproj_pass1<TagT, ACM_LAYOUT_AOS>), dim3(nb), dim3(kBlock), 0, s,
-                               prep(*cam), n, points_3d, points_2d, errs, p1);
-        else
-            hipLaunchKernelGGL((k_reproj_pass1<TagT, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s,
-                               prep(*cam), n, points_3d, points_2d, errs, p1);
-        hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb, tot);
-        hipLaunchKernelGGL(k_reproj_pass2, dim3(nb), dim3(kBlock), 0, s, n, errs, tot, p2);
-        hipLaunchKernelGGL(k_sum_columns, dim3(1), dim3(kBlock), 0, s, p2, nb, 1, var);
+        int nb1 = nb_max;
+        auto go = [&](auto lay_c) {
+            auto kern = k_reproj_pass1<TagT, decltype(lay_c)::value>;
+            nb1 = std::min(nb1, resident_blocks(reinterpret_cast<const void*>(kern)));
+            hipLaunchKernelGGL(kern, dim3(nb1), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
+                               points_2d, errs, p1);
+        };
+        if (layout == ACM_LAYOUT_AOS) go(std::integral_constant<int, ACM_LAYOUT_AOS>{});
+        else go(std::integral_constant<int, ACM_LAYOUT_SOA>{});
+        hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb1, tot);
+        hipLaunchKernelGGL(k_reproj_pass2, dim3(nb2), dim3(kBlock), 0, s, n, errs, tot, p2);
+        hipLaunchKernelGGL(k_sum_columns, dim3(1), dim3(kBlock), 0, s, p2, nb2, 1, var);
         hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, var, result);
         return check_launch("acm_reprojection_stats");
     });
@@ -1551,19 +1587,17 @@ ACM_API int acm_linear_system_qr(const acm_camera* cam, size_t n, const double* 
     if (workspace_bytes < acm_linear_system_qr_workspace_size(cam->model, n))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "linear-system workspace too small");
     hipStream_t s = (hipStream_t)stream;
-    const int nb = (int)tsqr_blocks(n);
     double* parts = (double*)workspace;
     if (hipMemsetAsync(error_flag, 0, sizeof(int), s) != hipSuccess)
         return check_launch("acm_linear_system_qr (memset)");
     auto go = [&](auto model_c) {
         constexpr int MOD = decltype(model_c)::value;
         constexpr int M = LinRows<MOD>::K + 1;
-        if (layout == ACM_LAYOUT_AOS)
-            hipLaunchKernelGGL((k_tsqr<MOD, ACM_LAYOUT_AOS>), dim3(nb), dim3(kBlock), 0, s, prep(*cam),
-                               n, points_3d, points_2d, parts, error_flag);
-        else
-            hipLaunchKernelGGL((k_tsqr<MOD, ACM_LAYOUT_SOA>), dim3(nb), dim3(kBlock), 0, s, prep(*cam),
-                               n, points_3d, points_2d, parts, error_flag);
+        auto kern = layout == ACM_LAYOUT_AOS ? k_tsqr<MOD, ACM_LAYOUT_AOS> : k_tsqr<MOD, ACM_LAYOUT_SOA>;
+        const int nb = std::min((int)tsqr_blocks(n),
+                                resident_blocks(reinterpret_cast<const void*>(kern)));
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
+                           points_2d, parts, error_flag);
         hipLaunchKernelGGL((k_tsqr_final<M>), dim3(1), dim3(kBlock), 0, s, parts, nb, r_factor);
     };
     switch (cam->model) {
@@ -1651,7 +1685,9 @@ ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
     SelState* sa = (SelState*)workspace;
     SelState* sb = sa + 1;
     double* hist = (double*)(sb + 1);
-    const unsigned nb = (unsigned)ne_blocks(n);
+    // <= 1024 workgroups: each flushes 256 histogram atomics per pass
+    const unsigned nb = (unsigned)std::min(
+        std::min(ne_blocks(n), 1024), resident_blocks(reinterpret_cast<const void*>(k_sel_hist)));
     for (int which = 0; which < 2; ++which) {
         SelState* st = which ? sb : sa;
         hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, s, st, n_valid_device,

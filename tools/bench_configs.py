@@ -141,8 +141,8 @@ def config3_ne_all(n):
                 res.setdefault(wv, []).append(timed(lambda: f.normal_equations(params, out)))
                 if rep == 0 and wv == 1:
                     ref = out.clone()
-                elif rep == 0:
-                    assert torch.equal(out, ref), "NE result depends on the waves target"
+                elif rep == 0:  # grid size follows occupancy -> summation order
+                    assert torch.allclose(out, ref, rtol=1e-12, atol=0.0)
         L.acm_set_tuning(_lib.TUNE_NE_WAVES, 3)
         ms = {wv: min(v) for wv, v in res.items()}
         best = min(ms, key=ms.get)
