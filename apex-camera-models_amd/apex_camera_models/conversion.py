@@ -24,6 +24,7 @@ class ConversionMetrics:
     convergence_status: str
     lm_iterations: int = 0
     lm_termination: str = ""
+    validation_results: object = None  # util.ValidationResults (validation.rs)
 
 
 # initial target parameters (camera_converter.rs:364-369, :500-505, :639-644,
@@ -88,11 +89,16 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
     final = reproj(model)
+    try:  # camera_converter.rs:425-438 (NaN results on failure)
+        validation = util.validate_conversion_accuracy(model, input_model)
+    except Exception:
+        validation = None
     return ConversionMetrics(model=model, model_name=DISPLAY[target],
                              final_reprojection_error=final, initial_reprojection_error=initial,
                              optimization_time_ms=ms, convergence_status=status,
                              lm_iterations=res.iterations if res else 0,
-                             lm_termination=res.termination if res else "")
+                             lm_termination=res.termination if res else "",
+                             validation_results=validation)
 
 
 def convert_all(input_model: CameraModel, num_points: int = 500,

@@ -127,3 +127,72 @@ def undistort_image(input_image, camera_model: CameraModel, target_intrinsics=No
                                                img.data_ptr(), out.data_ptr(),
                                                _stream_handle()))
     return out
+
+
+# ------------------------------------------------- validate_conversion_accuracy
+@dataclass
+class RegionValidation:
+    name: str
+    input_projection: object  # (u, v) or None
+    output_projection: object
+    error: float
+
+
+@dataclass
+class ValidationResults:
+    center_error: float
+    near_center_error: float
+    mid_region_error: float
+    edge_region_error: float
+    far_edge_error: float
+    average_error: float
+    max_error: float
+    status: str
+    region_data: list
+
+
+_REGIONS = (("Center", 0.5), ("Near Center", 0.55), ("Mid Region", 0.65),
+            ("Edge Region", 0.8), ("Far Edge", 0.95))
+
+
+def validate_conversion_accuracy(output_model: CameraModel,
+                                 input_model: CameraModel) -> ValidationResults:
+    """`validate_conversion_accuracy` (validation.rs:92-213): the five
+    diagonal test pixels (0.5 .. 0.95 of the input resolution) are
+    unprojected with the input model and the rays projected with both models
+    (one batched kernel call each); error = ||input_proj - output_proj||."""
+    import math
+    res = input_model.get_resolution()
+    w, h = float(res.width), float(res.height)
+    pix = torch.tensor([[w * f, h * f] for _, f in _REGIONS], dtype=torch.float64)
+    rays, st_u = input_model.unproject_batch(pix)
+    uv_in, st_in, _ = input_model.project_batch(rays)
+    uv_out, st_out, _ = output_model.project_batch(rays)
+    rays_ok = st_u.cpu().tolist()
+    ok_in, ok_out = st_in.cpu().tolist(), st_out.cpu().tolist()
+    a, b = uv_in.cpu().tolist(), uv_out.cpu().tolist()
+    total, max_error, valid = 0.0, 0.0, 0
+    errs, data = [], []
+    for i, (name, _) in enumerate(_REGIONS):
+        if rays_ok[i] == 0 and ok_in[i] == 0 and ok_out[i] == 0:  # :120-143
+            du, dv = a[i][0] - b[i][0], a[i][1] - b[i][1]
+            e = math.sqrt(du * du + dv * dv)
+            total += e
+            max_error = max(max_error, e)
+            valid += 1
+            errs.append(e)
+            data.append(RegionValidation(name, tuple(a[i]), tuple(b[i]), e))
+        else:  # :144-182: any failure -> NaN, no projections recorded
+            errs.append(float("nan"))
+            data.append(RegionValidation(name, None, None, float("nan")))
+    avg = total / valid if valid > 0 else float("nan")
+    if math.isnan(avg):  # :192-200
+        status = "NEEDS IMPROVEMENT"
+    elif avg < 0.001:
+        status = "EXCELLENT"
+    elif avg < 0.1:
+        status = "GOOD"
+    else:
+        status = "NEEDS IMPROVEMENT"
+    return ValidationResults(*errs, average_error=avg, max_error=max_error, status=status,
+                             region_data=data)

@@ -130,6 +130,8 @@ static int g_project_variant = -1;
 static int g_residual_nt = 0;
 // Normal equations: minimum waves per SIMD for the register allocator (1, 3, 4).
 static int g_ne_waves = 3;
+// FOV grid search: points per lane step (1, 2, 4).
+static int g_fov_unroll = 2;
 constexpr size_t kNtThresholdBytes = 256ull << 20;
 
 template <class TagT, int LAYOUT, bool WJ, bool NT>
@@ -1024,7 +1026,9 @@ constexpr int kFovGrid = ACM_FOV_GRID_SIZE;
 constexpr int kFovBlock = 320;
 constexpr int kFovMaxBlocks = 2048;
 
-template <int LAYOUT>
+// U: points evaluated per step of a lane (independent atan2 chains the
+// scheduler can interleave; the sum still adds them in point order).
+template <int LAYOUT, int U>
 __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n, size_t chunk,
                                                         const double* __restrict__ pts,
                                                         const double* __restrict__ obs,
@@ -1057,16 +1061,27 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n
         }
         __syncthreads();
         const int m = (int)(b1 - base < (size_t)kFovBlock ? b1 - base : (size_t)kFovBlock);
+        auto eval = [&](int k) -> double {
+            const double x = sx[k], y = sy[k], r2 = sr2[k];
+            const double atan_wrd = atan2(tw2 * sr[k], sz[k]);          // :196
+            const double rd = r2 < kEpsSqrt ? rd0 : atan_wrd / (sr[k] * w);  // :200-205
+            const double mx = x * rd, my = y * rd;
+            const double du = (fx * mx + cx) - su[k];
+            const double dv = (fy * my + cy) - sv[k];
+            return sqrt(du * du + dv * dv);  // :211-213
+        };
         if (active) {
-            for (int k = 0; k < m; ++k) {
-                const double x = sx[k], y = sy[k], r2 = sr2[k];
-                double rd;
-                if (r2 < kEpsSqrt) rd = rd0;  // :200-205 (uniform over the wave)
-                else rd = atan2(tw2 * sr[k], sz[k]) / (sr[k] * w);
-                const double mx = x * rd, my = y * rd;
-                const double du = (fx * mx + cx) - su[k];
-                const double dv = (fy * my + cy) - sv[k];
-                const double e = sqrt(du * du + dv * dv);  // :211-213
+            int k = 0;
+            for (; k + U <= m; k += U) {
+                double e[U];
+#pragma unroll
+                for (int j = 0; j < U; ++j) e[j] = eval(k + j);
+#pragma unroll
+                for (int j = 0; j < U; ++j)
+                    if (isfinite(e[j])) { sum += e[j]; cnt += 1.0; }
+            }
+            for (; k < m; ++k) {
+                const double e = eval(k);
                 if (isfinite(e)) { sum += e; cnt += 1.0; }
             }
         }
@@ -1657,12 +1672,20 @@ ACM_API int acm_fov_grid_errors(const acm_camera* cam, size_t n, const double* p
     if (hipMemcpyAsync(table, fov_grid_table(), 3 * kFovGrid * sizeof(double),
                        hipMemcpyHostToDevice, s) != hipSuccess)
         return check_launch("acm_fov_grid_errors (table)");
-    if (layout == ACM_LAYOUT_AOS)
-        hipLaunchKernelGGL((k_fov_grid<ACM_LAYOUT_AOS>), dim3(nb), dim3(kFovBlock), 0, s, *cam, n,
-                           chunk, points_3d, points_2d, table, parts);
-    else
-        hipLaunchKernelGGL((k_fov_grid<ACM_LAYOUT_SOA>), dim3(nb), dim3(kFovBlock), 0, s, *cam, n,
-                           chunk, points_3d, points_2d, table, parts);
+    auto go = [&](auto lay_c, auto u_c) {
+        hipLaunchKernelGGL((k_fov_grid<decltype(lay_c)::value, decltype(u_c)::value>), dim3(nb),
+                           dim3(kFovBlock), 0, s, *cam, n, chunk, points_3d, points_2d, table,
+                           parts);
+    };
+    auto by_unroll = [&](auto lay_c) {
+        switch (g_fov_unroll) {
+        case 1: go(lay_c, std::integral_constant<int, 1>{}); break;
+        case 4: go(lay_c, std::integral_constant<int, 4>{}); break;
+        default: go(lay_c, std::integral_constant<int, 2>{}); break;
+        }
+    };
+    if (layout == ACM_LAYOUT_AOS) by_unroll(std::integral_constant<int, ACM_LAYOUT_AOS>{});
+    else by_unroll(std::integral_constant<int, ACM_LAYOUT_SOA>{});
     hipLaunchKernelGGL(k_fov_finish, dim3((2 * kFovGrid + kBlock - 1) / kBlock), dim3(kBlock), 0,
                        s, parts, (int)nb, grid_sums);
     return check_launch("acm_fov_grid_errors");
@@ -1789,6 +1812,13 @@ ACM_API int acm_set_tuning(int key, int value) {
             return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 1, 3 or 4");
         const int old = g_ne_waves;
         g_ne_waves = value;
+        return old;
+    }
+    if (key == ACM_TUNE_FOV_UNROLL) {
+        if (value != 1 && value != 2 && value != 4)
+            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 1, 2 or 4");
+        const int old = g_fov_unroll;
+        g_fov_unroll = value;
         return old;
     }
     return fail(ACM_ERR_INVALID_ARGUMENT, "unknown tuning key");

@@ -359,8 +359,14 @@ ACM_API int acm_stream_synchronize(void *stream);
  * outputs exceed 256 MiB).  ACM_TUNE_RESIDUAL_NT: non-temporal stores in
  * acm_residual_jacobian (-1 auto, 0 off = default, 1 on).  ACM_TUNE_NE_WAVES:
  * minimum waves per SIMD the normal-equations kernel is compiled for
- * (1, 3 = default, 4).  Returns the previous value or an error. */
-enum { ACM_TUNE_PROJECT_VARIANT = 0, ACM_TUNE_RESIDUAL_NT = 1, ACM_TUNE_NE_WAVES = 2 };
+ * (1, 3 = default, 4).  ACM_TUNE_FOV_UNROLL: points per lane step of the FOV
+ * grid search (1, 2 = default, 4).  Returns the previous value or an error. */
+enum {
+    ACM_TUNE_PROJECT_VARIANT = 0,
+    ACM_TUNE_RESIDUAL_NT = 1,
+    ACM_TUNE_NE_WAVES = 2,
+    ACM_TUNE_FOV_UNROLL = 3
+};
 ACM_API int acm_set_tuning(int key, int value);
 
 /* Diagnostics: last HIP error code / message of the calling thread. */

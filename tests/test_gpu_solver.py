@@ -294,3 +294,38 @@ def test_conversion_kb_to_fov():
     assert met.model.NAME == "fov"
     assert met.final_reprojection_error.mean <= met.initial_reprojection_error.mean
     assert 1e-6 <= met.model.w <= 3.0
+
+
+@pytest.mark.parametrize("target", ["double_sphere", "ucm", "fov"])
+def test_validate_conversion_accuracy_matches_oracle(target):
+    """validation.rs:92-213 after a KB -> target conversion: the five region
+    errors recomputed with the oracle's unproject/project."""
+    import math
+
+    from apex_camera_models import KannalaBrandtModel, Resolution, conversion, util
+    params, (w, h) = SAMPLES[KB]
+    src = KannalaBrandtModel._from_params(params, Resolution(w, h))
+    uv, xyz = util.sample_points(src, 500)
+    met = conversion.convert(src, target, xyz, uv)
+    v = met.validation_results
+    assert v is not None and len(v.region_data) == 5
+    tid = met.model.MODEL_ID
+    out_p = met.model.params()
+    errs = []
+    for f in (0.5, 0.55, 0.65, 0.8, 0.95):
+        ray, su = O.unproject(KB, params, w, h, np.array([[w * f, h * f]]))
+        a, sa, _ = O.project(KB, params, w, h, ray)
+        b, sb, _ = O.project(tid, out_p, w, h, ray)
+        if su[0] == 0 and sa[0] == 0 and sb[0] == 0:
+            errs.append(math.hypot(*(a[0] - b[0])))
+        else:
+            errs.append(float("nan"))
+    got = [v.center_error, v.near_center_error, v.mid_region_error, v.edge_region_error,
+           v.far_edge_error]
+    for g_, e in zip(got, errs):
+        assert (math.isnan(g_) and math.isnan(e)) or abs(g_ - e) <= 1e-9 * max(1.0, e)
+    finite = [e for e in errs if not math.isnan(e)]
+    assert v.max_error == pytest.approx(max(finite) if finite else 0.0, abs=1e-9)
+    assert v.status in ("EXCELLENT", "GOOD", "NEEDS IMPROVEMENT")
+    if target == "double_sphere":
+        assert v.status in ("EXCELLENT", "GOOD")

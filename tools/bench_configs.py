@@ -162,7 +162,21 @@ def config_fov(n_target):
     uv, xyz = util.sample_points(src, n_target)
     n = xyz.shape[0]
     m = conversion._init_target("fov", src)
-    ms = timed(lambda: m.linear_estimation(xyz, uv), reps=3, warm=1)
+    from apex_camera_models import _lib
+    L = _lib.load()
+    by = {}
+    for rep in range(2):  # interleaved A/B of the per-lane unroll
+        for u in (1, 2, 4):
+            L.acm_set_tuning(_lib.TUNE_FOV_UNROLL, u)
+            m.w = 1.0
+            by.setdefault(u, []).append(timed(lambda: m.linear_estimation(xyz, uv), reps=3,
+                                              warm=1))
+            by.setdefault(("w", u), []).append(m.w)
+    L.acm_set_tuning(_lib.TUNE_FOV_UNROLL, 2)
+    assert len({v[0] for k, v in by.items() if isinstance(k, tuple)}) == 1
+    ms = min(min(by[u]) for u in (1, 2, 4))
+    emit({"config": "fov", "what": "FOV grid unroll A/B",
+          "ms_by_unroll": {str(u): round(min(by[u]), 3) for u in (1, 2, 4)}})
     met = conversion.convert(src, "fov", xyz, uv)
     emit({"config": "fov", "what": "FOV grid-search linear estimation", "points": n,
           "ms": round(ms, 3), "evaluations_per_s": round(290 * n / ms / 1e3, 1), "w": m.w,
