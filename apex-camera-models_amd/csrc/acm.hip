@@ -128,8 +128,15 @@ static int g_project_variant = -1;
 // measured slower here (DS, 9.3M points: 0.273 ms plain vs 0.310 ms nt,
 // profiles/r01_configs.log); -1 = auto (nt above kNtThresholdBytes), 1 = on.
 static int g_residual_nt = 0;
-// Normal equations: minimum waves per SIMD for the register allocator (1, 3, 4).
-static int g_ne_waves = 3;
+// Normal equations: minimum waves per SIMD for the register allocator (1, 3,
+// 4) and points per lane step (1, 2, 4); 0 = the per-model default below.
+static int g_ne_waves = 0;
+static int g_ne_unroll = 0;
+// +J launches: -1 = auto = k_project_al (line-aligned store windows; as fast
+// as k_project for N a multiple of 8 and 30-45% faster otherwise,
+// profiles/r01_diag_align.log), 0 = k_project / k_residual, 1 = k_project_al,
+// 2 = k_project_al with 248-point windows (A/B only: 15% slower).
+static int g_align_j = -1;
 // FOV grid search: points per lane step (1, 2, 4).
 static int g_fov_unroll = 2;
 constexpr size_t kNtThresholdBytes = 256ull << 20;
@@ -221,6 +228,149 @@ __global__ __launch_bounds__(kBlock) void k_project_f32(acm_camera cam, size_t n
 #pragma unroll
         for (int p = 0; p < P; ++p) put(jac + p * col + 2 * i, ok ? ju[p] : 0.0f, ok ? jv[p] : 0.0f);
     }
+}
+
+// ------------------------------------------ line-aligned Jacobian stores
+// Column c of the 2N x P column-major Jacobian starts at byte 16*c*N.  Unless
+// N is a multiple of 8, every wave's 1 KiB slice of a column straddles two
+// 128-B lines that other workgroups (on other XCDs) complete at another
+// time, and those partial-line writes cost HBM efficiency: the same traffic
+// runs at 4.6-5.1 TB/s with 16/32-B-misaligned columns vs 6.7-7.2 TB/s
+// aligned (tools/diag_align.py, profiles/r01_diag_align.log; the real kernel
+// and a zero-compute mimic alike).  k_project_al makes every store window
+// line-aligned whatever N and the buffer offsets are: workgroup b owns
+// points [248b, 248b + 248) (lanes 0..247) and lanes 248..255 also project
+// the 8 points before them.  A stream whose elements sit s (0..7) 16-B
+// elements off the line grid is written by lane t as element 248b - s + t,
+// so each 128-B line of it is written whole by one workgroup; the value
+// comes from lane t - s, or from lead-in lane 256 - s + t for t < s, through
+// LDS.  Streams already on the grid (s = 0) are stored straight from
+// registers.  BASE_AL: uv / residual and J column 0 are on the grid (the
+// buffers start on a 128-B line, as every torch / hipMalloc buffer does), so
+// only columns 1..P-1 go through LDS (KB: 18.7 KB per workgroup, 8 per CU).
+// The lead-in costs 3% extra math and 8 x 24 B of re-read per workgroup.
+// Results are bit-identical to k_project / k_residual (same per-point code).
+// Every model's J rows are u [a, 0, 1, 0, du..], v [0, b, 0, 1, dv..]
+// (camera_models.hpp), so LDS holds a, b, validity and the D distortion
+// pairs, not all 2P values.
+// OWN = points a workgroup owns: 248 (lanes 248..255 project the lead-in) or
+// 256 (lanes 0..7 project a second, lead-in point); window chunks of 256
+// keep each wave's 1 KiB column slices on the same 1 KiB grid as k_project.
+constexpr int kAlLead = 8;
+
+__device__ __forceinline__ unsigned misalign16(const void* p, size_t elem_offset) {
+    return (unsigned)(((reinterpret_cast<uintptr_t>(p) >> 4) + elem_offset) & 7u);
+}
+
+template <class TagT, int LAYOUT, bool RESID, bool BASE_AL, int OWN>
+__global__ __launch_bounds__(kBlock) void k_project_al(acm_camera cam, size_t n,
+                                                       const double* __restrict__ pts,
+                                                       const double* __restrict__ obs,
+                                                       int policy, double* __restrict__ out2,
+                                                       uint8_t* __restrict__ status,
+                                                       double* __restrict__ jac) {
+    static_assert(OWN == kBlock || OWN == kBlock - kAlLead, "OWN");
+    using M = typename TagT::template type<double>;
+    constexpr int P = M::P;
+    constexpr int D = P - 4;
+    constexpr int S = OWN + kAlLead;          // LDS slots: own points, then the lead-in
+    constexpr int NW = BASE_AL ? 1 : S;       // s_uv / s_a only when they can be shifted
+    __shared__ double2 s_uv[NW];
+    __shared__ double s_a[NW];
+    __shared__ double s_b[S];
+    __shared__ double2 s_d[D > 0 ? D : 1][S];
+    __shared__ uint8_t s_ok[S];
+    const Cam<double> c = make_cam<double>(cam);
+    const int t = threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * OWN;
+    auto eval = [&](size_t p, bool have, int slot, bool own) {
+        double x = 0.0, y = 0.0, z = 1.0;
+        if (have) load_point<LAYOUT>(pts, n, p, x, y, z);
+        double u, v, ju[P], jv[P];
+        const uint8_t st = M::template project<true>(c, x, y, z, u, v, ju, jv);
+        const bool ok = have && st == ST_OK;
+        double2 w;
+        if (RESID) {
+            double2 o = make_double2(0.0, 0.0);
+            if (have) o = *reinterpret_cast<const double2*>(obs + 2 * p);
+            const double sent = policy == ACM_INVALID_SENTINEL ? 1e6 : 0.0;
+            w = make_double2(ok ? u - o.x : sent, ok ? v - o.y : sent);
+        } else {
+            w = make_double2(ok ? u : __builtin_nan(""), ok ? v : __builtin_nan(""));
+        }
+        const double a0 = ok ? ju[0] : 0.0;
+        if (BASE_AL) {
+            if (own && have) {
+                st2<true>(out2 + 2 * p, w.x, w.y);
+                st2<true>(jac + 2 * p, a0, 0.0);
+            }
+        } else {
+            s_uv[slot] = w;
+            s_a[slot] = a0;
+        }
+        s_b[slot] = ok ? jv[1] : 0.0;
+        s_ok[slot] = ok;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+            s_d[k][slot] = make_double2(ok ? ju[4 + k] : 0.0, ok ? jv[4 + k] : 0.0);
+        if (status && own && have) st1<true>(status + p, st);
+    };
+    // lead-in point k (0..7) = base - 8 + k, in slot OWN + k
+    if (OWN == kBlock) {
+        eval(base + t, base + t < n, t, true);
+        if (t < kAlLead) eval(base + t - kAlLead, base >= (size_t)kAlLead, OWN + t, false);
+    } else if (t < OWN) {
+        eval(base + t, base + t < n, t, true);
+    } else {
+        eval(base + t - kBlock, base >= (size_t)kAlLead, t, false);
+    }
+    __syncthreads();
+    if (t >= OWN) return;
+    // element base - sh + t of a stream sitting sh elements off the line grid:
+    // own point base + t - sh (slot t - sh) or lead-in slot S - sh + t
+    size_t e;
+    int j;
+    auto elem = [&](unsigned sh) {
+        j = t >= (int)sh ? t - (int)sh : S - (int)sh + t;
+        e = base + t - sh;
+        return base + t >= sh && e < n;
+    };
+    if (!BASE_AL && elem(misalign16(out2, 0))) st2<true>(out2 + 2 * e, s_uv[j].x, s_uv[j].y);
+#pragma unroll
+    for (int col = BASE_AL ? 1 : 0; col < P; ++col) {
+        if (!elem(misalign16(jac, (size_t)col * n))) continue;
+        double va, vb;
+        if (col == 0) { va = s_a[j]; vb = 0.0; }
+        else if (col == 1) { va = 0.0; vb = s_b[j]; }
+        else if (col == 2) { va = s_ok[j] ? 1.0 : 0.0; vb = 0.0; }
+        else if (col == 3) { va = 0.0; vb = s_ok[j] ? 1.0 : 0.0; }
+        else { va = s_d[col - 4][j].x; vb = s_d[col - 4][j].y; }
+        st2<true>(jac + (size_t)col * 2 * n + 2 * e, va, vb);
+    }
+}
+
+// uv / residual and J column 0 on the 128-B grid (k_project_al<.., BASE_AL>)
+static bool al_base_aligned(const void* out2, const double* jac) {
+    return (reinterpret_cast<uintptr_t>(out2) & 127u) == 0 &&
+           (reinterpret_cast<uintptr_t>(jac) & 127u) == 0;
+}
+
+// workgroups so that the last window [B*OWN - s, ...) reaches n for every s <= 7
+static unsigned al_blocks(size_t n, int own) { return (unsigned)((n + kAlLead - 1 + own) / own); }
+
+// g_align_j: 2 forces the OWN = 248 variant (A/B), anything else uses 256.
+template <class TagT, int LAY, bool RESID>
+static void launch_al(hipStream_t s, const acm_camera& cam, size_t n, const double* pts,
+                      const double* obs, int policy, double* out2, uint8_t* status,
+                      double* jac) {
+    const bool bal = al_base_aligned(out2, jac);
+    const int own = g_align_j == 2 ? kBlock - kAlLead : kBlock;
+    auto kern = bal ? (own == kBlock ? k_project_al<TagT, LAY, RESID, true, kBlock>
+                                     : k_project_al<TagT, LAY, RESID, true, kBlock - kAlLead>)
+                    : (own == kBlock ? k_project_al<TagT, LAY, RESID, false, kBlock>
+                                     : k_project_al<TagT, LAY, RESID, false, kBlock - kAlLead>);
+    hipLaunchKernelGGL(kern, dim3(al_blocks(n, own)), dim3(kBlock), 0, s, cam, n, pts, obs,
+                       policy, out2, status, jac);
 }
 
 // --------------------------------------------------------------- unproject
@@ -354,6 +504,16 @@ struct NE {
     static constexpr int K = G + 4 + D + 2;
 };
 
+// Per-model (waves, points per lane step) of k_normal_eq: the fastest cell of
+// the interleaved {1,3,4} x {1,2,4} sweep (tools/bench_configs.py --configs
+// 3ne, profiles/r01_ne_sweep.log, 10M points).  All cells give the same sums
+// up to summation order.
+template <class TagT> struct NeDefault { static constexpr int W = 3, U = 1; };
+template <> struct NeDefault<Tag<Pinhole>> { static constexpr int W = 3, U = 4; };
+template <> struct NeDefault<Tag<RadTan>> { static constexpr int W = 1, U = 2; };
+template <> struct NeDefault<Tag<DoubleSphere>> { static constexpr int W = 4, U = 2; };
+template <> struct NeDefault<Tag<Eucm>> { static constexpr int W = 4, U = 2; };
+
 constexpr int kNeMaxBlocks = 2048;  // reprojection stats / median partials
 constexpr int kNqMaxBlocks = 2048;  // normal equations: 8 workgroups per CU
 
@@ -401,7 +561,7 @@ static int resident_blocks(const void* kernel) {
 // (amdgpu_waves_per_eu).  1 leaves it free (KB lands at 176 VGPRs = 2 waves);
 // 3 fits KB in 168 without spills; 4 forces 128 with scratch spills for KB and
 // RadTan.  Selected per launch by ACM_TUNE_NE_WAVES (results identical).
-template <class TagT, int LAYOUT, int WAVES>
+template <class TagT, int LAYOUT, int WAVES, int U>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq(acm_camera cam, size_t n,
                                                       const double* __restrict__ pts,
                                                       const double* __restrict__ obs, int policy,
@@ -418,34 +578,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
     const size_t stride = (size_t)gridDim.x * kBlock;
     size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    // software pipeline: the next point's 40 bytes are in flight while the
-    // current one is projected and accumulated.  Not for the largest
-    // accumulator sets (KB, RadTan), where the extra 10 VGPRs cost a wave of
-    // occupancy.
+    // Software pipeline: the next U points' 40 bytes each are in flight while
+    // the current U are projected and accumulated (U points per lane step,
+    // ACM_TUNE_NE_UNROLL).  Not for the largest accumulator sets (KB,
+    // RadTan), where the extra registers cost a wave of occupancy.
     constexpr bool kPrefetch = K <= 40;
-    double x = 0, y = 0, z = 1;
-    double2 o = make_double2(0.0, 0.0);
-    if (kPrefetch && i < n) {
-        load_point<LAYOUT>(pts, n, i, x, y, z);
-        o = *reinterpret_cast<const double2*>(obs + 2 * i);
-    }
-    for (; i < n; i += stride) {
-        const size_t inext = i + stride;
-        double xn = 0, yn = 0, zn = 1;
-        double2 on = make_double2(0.0, 0.0);
-        if (kPrefetch) {
-            if (inext < n) {
-                load_point<LAYOUT>(pts, n, inext, xn, yn, zn);
-                on = *reinterpret_cast<const double2*>(obs + 2 * inext);
-            }
-        } else {
-            load_point<LAYOUT>(pts, n, i, x, y, z);
-            o = *reinterpret_cast<const double2*>(obs + 2 * i);
-        }
+    auto accumulate = [&](double px, double py, double pz, double2 po) {
         double u, v, ju[P], jv[P];
-        const uint8_t st = M::template project<true>(c, x, y, z, u, v, ju, jv);
+        const uint8_t st = M::template project<true>(c, px, py, pz, u, v, ju, jv);
         if (st == ST_OK) {
-            const double r0 = u - o.x, r1 = v - o.y;
+            const double r0 = u - po.x, r1 = v - po.y;
             const double a = ju[0], b = jv[1];
             acc[0] += a * a;
             acc[1] += a;
@@ -475,7 +617,58 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         } else {
             acc[K - 2] += sent2;
         }
-        if (kPrefetch) { x = xn; y = yn; z = zn; o = on; }
+    };
+    if constexpr (U == 1) {
+        double x = 0, y = 0, z = 1;
+        double2 o = make_double2(0.0, 0.0);
+        if (kPrefetch && i < n) {
+            load_point<LAYOUT>(pts, n, i, x, y, z);
+            o = *reinterpret_cast<const double2*>(obs + 2 * i);
+        }
+        for (; i < n; i += stride) {
+            const size_t inext = i + stride;
+            double xn = 0, yn = 0, zn = 1;
+            double2 on = make_double2(0.0, 0.0);
+            if (kPrefetch) {
+                if (inext < n) {
+                    load_point<LAYOUT>(pts, n, inext, xn, yn, zn);
+                    on = *reinterpret_cast<const double2*>(obs + 2 * inext);
+                }
+            } else {
+                load_point<LAYOUT>(pts, n, i, x, y, z);
+                o = *reinterpret_cast<const double2*>(obs + 2 * i);
+            }
+            accumulate(x, y, z, o);
+            if (kPrefetch) { x = xn; y = yn; z = zn; o = on; }
+        }
+    } else {
+        double x[U], y[U], z[U], xn[U], yn[U], zn[U];
+        double2 o[U], on[U];
+        auto load = [&](size_t base, double (&xs)[U], double (&ys)[U], double (&zs)[U],
+                        double2 (&os)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const size_t j = base + (size_t)u * stride;
+                xs[u] = 0.0; ys[u] = 0.0; zs[u] = 1.0;
+                os[u] = make_double2(0.0, 0.0);
+                if (j < n) {
+                    load_point<LAYOUT>(pts, n, j, xs[u], ys[u], zs[u]);
+                    os[u] = *reinterpret_cast<const double2*>(obs + 2 * j);
+                }
+            }
+        };
+        if (kPrefetch) load(i, x, y, z, o);
+        for (; i < n; i += (size_t)U * stride) {
+            if (kPrefetch) load(i + (size_t)U * stride, xn, yn, zn, on);
+            else load(i, x, y, z, o);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (u == 0 || i + (size_t)u * stride < n) accumulate(x[u], y[u], z[u], o[u]);
+            if (kPrefetch) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) { x[u] = xn[u]; y[u] = yn[u]; z[u] = zn[u]; o[u] = on[u]; }
+            }
+        }
     }
     block_sum_store<K>(acc, parts + (size_t)blockIdx.x * K);
 }
@@ -1274,6 +1467,21 @@ ACM_API int acm_project(const acm_camera* cam, size_t n, const double* points_3d
             n * (17 + (jacobian ? 16 * (size_t)acm_num_params(cam->model) : 0));
         var = out_bytes > kNtThresholdBytes ? kVarNT : 0;
     }
+    const int P = acm_num_params(cam->model);
+    (void)P;
+    const bool align = jacobian && g_align_j != 0;
+    if (align) {  // line-aligned store windows (always non-temporal: measured faster)
+        return dispatch_model(cam->model, [&](auto tag) -> int {
+            using TagT = decltype(tag);
+            if (layout == ACM_LAYOUT_AOS)
+                launch_al<TagT, ACM_LAYOUT_AOS, false>(s, prep(*cam), n, points_3d, nullptr, 0,
+                                                       points_2d, status, jacobian);
+            else
+                launch_al<TagT, ACM_LAYOUT_SOA, false>(s, prep(*cam), n, points_3d, nullptr, 0,
+                                                       points_2d, status, jacobian);
+            return check_launch("acm_project");
+        });
+    }
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
         auto launch = [&](auto lay_c, auto wj_c, auto var_c) {
@@ -1377,6 +1585,16 @@ ACM_API int acm_residual_jacobian(const acm_camera* cam, size_t n, const double*
         const size_t out_bytes =
             n * (17 + (jacobian ? 16 * (size_t)acm_num_params(cam->model) : 0));
         const bool nt = g_residual_nt < 0 ? out_bytes > kNtThresholdBytes : g_residual_nt == 1;
+        const bool align = jacobian && g_align_j != 0;
+        if (align) {  // line-aligned store windows (always non-temporal: measured faster)
+            if (layout == ACM_LAYOUT_AOS)
+                launch_al<TagT, ACM_LAYOUT_AOS, true>(s, prep(*cam), n, points_3d, points_2d_obs,
+                                                      invalid_policy, residual, status, jacobian);
+            else
+                launch_al<TagT, ACM_LAYOUT_SOA, true>(s, prep(*cam), n, points_3d, points_2d_obs,
+                                                      invalid_policy, residual, status, jacobian);
+            return check_launch("acm_residual_jacobian");
+        }
 #define ACM_LAUNCH_RES(L, WJ)                                                                   \
     do {                                                                                        \
         if (nt)                                                                                 \
@@ -1430,15 +1648,21 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
         double* parts = (double*)workspace;
         double* sums = parts + (size_t)nb_max * K;
         int nb = nb_max;
+        using Def = NeDefault<TagT>;
+        const int wv = g_ne_waves ? g_ne_waves : Def::W;
+        const int un = g_ne_unroll ? g_ne_unroll : Def::U;
         auto go = [&](auto lay_c, auto w_c) {
-            auto kern = k_normal_eq<TagT, decltype(lay_c)::value, decltype(w_c)::value>;
+            constexpr int LAY = decltype(lay_c)::value, W = decltype(w_c)::value;
+            auto kern = k_normal_eq<TagT, LAY, W, 1>;
+            if (un == 2) kern = k_normal_eq<TagT, LAY, W, 2>;
+            if (un == 4) kern = k_normal_eq<TagT, LAY, W, 4>;
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
                                points_2d_obs, invalid_policy, parts);
         };
         auto by_waves = [&](auto lay_c) {
-            switch (g_ne_waves) {
+            switch (wv) {
             case 1: go(lay_c, std::integral_constant<int, 1>{}); break;
             case 4: go(lay_c, std::integral_constant<int, 4>{}); break;
             default: go(lay_c, std::integral_constant<int, 3>{}); break;
@@ -1808,10 +2032,23 @@ ACM_API int acm_set_tuning(int key, int value) {
         return old;
     }
     if (key == ACM_TUNE_NE_WAVES) {
-        if (value != 1 && value != 3 && value != 4)
-            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 1, 3 or 4");
+        if (value != 0 && value != 1 && value != 3 && value != 4)
+            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 0 (per-model default), 1, 3 or 4");
         const int old = g_ne_waves;
         g_ne_waves = value;
+        return old;
+    }
+    if (key == ACM_TUNE_NE_UNROLL) {
+        if (value != 0 && value != 1 && value != 2 && value != 4)
+            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 0 (per-model default), 1, 2 or 4");
+        const int old = g_ne_unroll;
+        g_ne_unroll = value;
+        return old;
+    }
+    if (key == ACM_TUNE_ALIGN_J) {
+        if (value < -1 || value > 2) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..2");
+        const int old = g_align_j;
+        g_align_j = value;
         return old;
     }
     if (key == ACM_TUNE_FOV_UNROLL) {

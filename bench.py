@@ -79,6 +79,64 @@ def cpu_baseline(model_id, params, w, h, n, seconds):
                       f"-ffp-contract=off, 1 thread"}
 
 
+def host_threads():
+    """CPU threads this process may use: its affinity set, capped at 16 (the
+    GPU box's per-GPU CPU share; os.cpu_count() there shows the whole host)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return max(1, min(16, avail))
+
+
+def cpu_baseline_all_cores(model_id, params, w, h, n, seconds, threads):
+    """The same oracle loop on `threads` host threads (disjoint contiguous
+    chunks of the 10M-point batch, each with its own output buffers; ctypes
+    drops the GIL for the C call), SURVEY.md §8(d)'s "and with all host
+    cores" leg.  Median throughput of whole-batch passes."""
+    import threading
+
+    import numpy as np
+
+    import oracle
+    from apex_camera_models import samples
+    pts = samples.synthetic_points(n)
+    P = oracle.NUM_PARAMS[model_id]
+    L = oracle.lib()
+    dp = oracle._dp
+    pa = np.ascontiguousarray(params, dtype=np.float64)
+    bounds = [(n * t // threads, n * (t + 1) // threads) for t in range(threads)]
+    bufs = []
+    for s, e in bounds:
+        m = e - s
+        bufs.append((np.ascontiguousarray(pts[s:e]), np.empty((m, 2)),
+                     np.empty(m, dtype=np.uint8), np.empty((P, m, 2))))
+
+    def work(t):
+        x, uv, st, jac = bufs[t]
+        L.oracle_project_batch(model_id, dp(pa), w, h, len(x), dp(x), dp(uv),
+                               oracle._u8p(st), dp(jac))
+
+    rates, t_total = [], 0.0
+    while t_total < seconds or len(rates) < 3:
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t0
+        t_total += dt
+        rates.append(n / dt / 1e6)
+        if len(rates) >= 200:
+            break
+    rates.sort()
+    return {"value": rates[len(rates) // 2], "unit": "Mpoints/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{len(rates)} x full {n}-point batch (project + 2x{P} J) split over "
+                      f"{threads} threads, {t_total:.1f} s wall, median; same oracle build"}
+
+
 def load_traffic(workload, n):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this
     exact workload (profiles/*pmc*.json, written by profiles/collect_pmc.py),
@@ -207,6 +265,10 @@ def main():
         if not a.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(model_id, params, w, h, n,
                                                a.cpu_baseline_seconds)
+            thr = host_threads()
+            if thr > 1:
+                res["cpu_baseline_all_cores"] = cpu_baseline_all_cores(
+                    model_id, params, w, h, n, a.cpu_baseline_seconds / 2, thr)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()

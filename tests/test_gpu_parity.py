@@ -164,6 +164,41 @@ def test_normal_equations_vs_oracle(golden_dir, model, policy):
 
 
 @pytest.mark.parametrize("model", range(7))
+def test_normal_equations_every_tuning_cell(model):
+    """Every (waves, points-per-lane-step) cell of k_normal_eq on a ragged
+    batch several grid strides long (exercises the unrolled tails) agrees
+    with the oracle; the knobs only change the summation order."""
+    import torch
+    from apex_camera_models import _lib, factors, samples
+    from apex_camera_models.camera import Resolution
+    params, (w, h) = samples.SAMPLES[model]
+    n = 1_234_567
+    xyz = samples.synthetic_points(n)
+    xyz = xyz[np.isfinite(xyz).all(1)]
+    uv0, st0, _ = O.project(model, params, w, h, xyz)
+    obs = np.where(np.isnan(uv0), 3.0, uv0) + 0.25
+    A0, b0, c0, nv0 = O.normal_equations(model, params, w, h, xyz, obs, 0)
+    f = factors.CameraParamsFactor.__subclasses__()[model](
+        torch.as_tensor(xyz), torch.as_tensor(obs), Resolution(w, h))
+    P = len(params)
+    L = _lib.load()
+    try:
+        for wv in (0, 1, 3, 4):
+            for un in (0, 1, 2, 4):
+                L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)
+                L.acm_set_tuning(_lib.TUNE_NE_UNROLL, un)
+                res = f.normal_equations(params)
+                A, b, c, nv = [t.cpu().numpy() for t in f.unpack_normal_equations(res, P)]
+                assert int(nv) == nv0, (wv, un)
+                assert np.abs(A - A0).max() <= TOL * np.abs(A0).max(), (wv, un)
+                assert np.abs(b - b0).max() <= TOL * max(np.abs(b0).max(), 1.0), (wv, un)
+                assert abs(c - c0) <= TOL * max(abs(c0), 1.0), (wv, un)
+    finally:
+        L.acm_set_tuning(_lib.TUNE_NE_WAVES, 0)
+        L.acm_set_tuning(_lib.TUNE_NE_UNROLL, 0)
+
+
+@pytest.mark.parametrize("model", range(7))
 def test_reprojection_error_vs_oracle(golden_dir, model):
     import torch
     from apex_camera_models import util

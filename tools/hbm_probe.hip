@@ -1,0 +1,99 @@
+// hbm_probe.hip -- zero-compute HBM ceilings for the hot path's access
+// patterns (a measuring tool, not part of libacm.so).
+//
+//   acm_probe_read   : grid-stride sum of a buffer (the normal-equations
+//                      kernel's pure 40 B/pt read stream, no math)
+//   acm_probe_write  : fill a buffer with 16-B stores (plain or nt)
+//   acm_probe_mimic  : the exact traffic of k_project<*, J>: read 24 B/pt
+//                      (AoS xyz), write 16 B uv + 1 B status + `cols` 16-B
+//                      Jacobian column pairs (2N x cols column-major), with a
+//                      trivial function of the inputs instead of the camera
+//                      model -- the same bytes, in the same instruction shape,
+//                      with (almost) no VALU work.
+//
+// Built by tools/Makefile (hipcc --offload-arch=gfx950); driven by
+// tools/hbm_ceiling.py.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ void put2(double* p, double a, double b) {
+    dbl2 v = {a, b};
+    if (NT) __builtin_nontemporal_store(v, reinterpret_cast<dbl2*>(p));
+    else *reinterpret_cast<dbl2*>(p) = v;
+}
+
+__global__ __launch_bounds__(256) void k_read(const dbl2* __restrict__ p, size_t n2,
+                                              double* __restrict__ out) {
+    // one partial per wave (no same-address atomics: they would serialise)
+    double s = 0.0;
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + stride < n2; i += 2 * stride) {
+        const dbl2 a = p[i], b = p[i + stride];
+        s += a.x + a.y + b.x + b.y;
+    }
+    if (i < n2) { const dbl2 a = p[i]; s += a.x + a.y; }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) out[(size_t)blockIdx.x * 4 + (threadIdx.x >> 6)] = s;
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void k_write(double* __restrict__ p, size_t n2, double v) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n2) put2<NT>(p + 2 * i, v, v);
+}
+
+template <bool NT, int COLS>
+__global__ __launch_bounds__(256) void k_mimic(size_t n, const double* __restrict__ xyz,
+                                               double* __restrict__ uv, uint8_t* __restrict__ st,
+                                               double* __restrict__ jac) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    put2<NT>(uv + 2 * i, x + z, y + z);
+    if (NT) __builtin_nontemporal_store((uint8_t)(z < 0.0), st + i);
+    else st[i] = (uint8_t)(z < 0.0);
+#pragma unroll
+    for (int c = 0; c < COLS; ++c) put2<NT>(jac + (size_t)c * 2 * n + 2 * i, x * c, y * c);
+}
+
+static unsigned blocks(size_t n) { return (unsigned)((n + 255) / 256); }
+
+extern "C" {
+
+int acm_probe_read(const void* buf, size_t bytes, double* out, int grid, void* stream) {
+    const size_t n2 = bytes / 16;
+    hipLaunchKernelGGL(k_read, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const dbl2*)buf, n2, out);
+    return (int)hipGetLastError();
+}
+
+int acm_probe_write(void* buf, size_t bytes, int nt, void* stream) {
+    const size_t n2 = bytes / 16;
+    if (nt) hipLaunchKernelGGL(k_write<true>, dim3(blocks(n2)), dim3(256), 0, (hipStream_t)stream,
+                               (double*)buf, n2, 1.0);
+    else hipLaunchKernelGGL(k_write<false>, dim3(blocks(n2)), dim3(256), 0, (hipStream_t)stream,
+                            (double*)buf, n2, 1.0);
+    return (int)hipGetLastError();
+}
+
+int acm_probe_mimic(size_t n, const double* xyz, double* uv, uint8_t* st, double* jac, int cols,
+                    int nt, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+#define MIMIC(C)                                                                          \
+    if (cols == C) {                                                                      \
+        if (nt) hipLaunchKernelGGL((k_mimic<true, C>), dim3(blocks(n)), dim3(256), 0, s, n, \
+                                   xyz, uv, st, jac);                                     \
+        else hipLaunchKernelGGL((k_mimic<false, C>), dim3(blocks(n)), dim3(256), 0, s, n,  \
+                                xyz, uv, st, jac);                                        \
+        return (int)hipGetLastError();                                                    \
+    }
+    MIMIC(0) MIMIC(4) MIMIC(5) MIMIC(6) MIMIC(8) MIMIC(9)
+#undef MIMIC
+    return -1;
+}
+
+}  // extern "C"
