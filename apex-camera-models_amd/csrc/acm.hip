@@ -82,17 +82,35 @@ __device__ __forceinline__ Cam<T> make_cam(const acm_camera& c) {
     return k;
 }
 
-template <int LAYOUT>
+// NTL: non-temporal loads (read-once streams; the read probe measured 6.9 vs
+// 6.3 TB/s for a 400 MB sweep, profiles/r01_hbm_ceiling.log)
+template <bool NTL>
+__device__ __forceinline__ double ld1(const double* p) {
+    if (NTL) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+template <bool NTL>
+__device__ __forceinline__ double2 ld2(const double* p) {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    if (NTL) {
+        const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
+        return make_double2(v.x, v.y);
+    }
+    return *reinterpret_cast<const double2*>(p);
+}
+
+template <int LAYOUT, bool NTL = false>
 __device__ __forceinline__ void load_point(const double* __restrict__ pts, size_t n, size_t i,
                                            double& x, double& y, double& z) {
     if (LAYOUT == ACM_LAYOUT_AOS) {
-        x = pts[3 * i];
-        y = pts[3 * i + 1];
-        z = pts[3 * i + 2];
+        x = ld1<NTL>(pts + 3 * i);
+        y = ld1<NTL>(pts + 3 * i + 1);
+        z = ld1<NTL>(pts + 3 * i + 2);
     } else {
-        x = pts[i];
-        y = pts[n + i];
-        z = pts[2 * n + i];
+        x = ld1<NTL>(pts + i);
+        y = ld1<NTL>(pts + n + i);
+        z = ld1<NTL>(pts + 2 * n + i);
     }
 }
 
@@ -134,9 +152,12 @@ static int g_ne_waves = 0;
 static int g_ne_unroll = 0;
 // +J launches: -1 = auto = k_project_al (line-aligned store windows; as fast
 // as k_project for N a multiple of 8 and 30-45% faster otherwise,
-// profiles/r01_diag_align.log), 0 = k_project / k_residual, 1 = k_project_al,
-// 2 = k_project_al with 248-point windows (A/B only: 15% slower).
+// profiles/r01_diag_align.log), 0 = k_project / k_residual, 1 = k_project_al.
 static int g_align_j = -1;
+// Non-temporal loads of the read-once point / observation streams in
+// k_normal_eq: -1 = auto (on), 0 = off, 1 = on (5-11% faster, read probe
+// 6.9 vs 6.3 TB/s; profiles/r01_ne_sweep.log, r01_hbm_ceiling.log).
+static int g_nt_loads = -1;
 // FOV grid search: points per lane step (1, 2, 4).
 static int g_fov_unroll = 2;
 constexpr size_t kNtThresholdBytes = 256ull << 20;
@@ -253,27 +274,28 @@ __global__ __launch_bounds__(kBlock) void k_project_f32(acm_camera cam, size_t n
 // Every model's J rows are u [a, 0, 1, 0, du..], v [0, b, 0, 1, dv..]
 // (camera_models.hpp), so LDS holds a, b, validity and the D distortion
 // pairs, not all 2P values.
-// OWN = points a workgroup owns: 248 (lanes 248..255 project the lead-in) or
-// 256 (lanes 0..7 project a second, lead-in point); window chunks of 256
-// keep each wave's 1 KiB column slices on the same 1 KiB grid as k_project.
+// Each workgroup owns 256 points (lanes 0..7 also project one lead-in point
+// each): window chunks of 256 keep each wave's 1 KiB column slices on the
+// same 1 KiB grid as k_project (248-point windows measured 15% slower,
+// profiles/r01_diag_align.log).
 constexpr int kAlLead = 8;
+constexpr int kAlOwn = kBlock;
 
 __device__ __forceinline__ unsigned misalign16(const void* p, size_t elem_offset) {
     return (unsigned)(((reinterpret_cast<uintptr_t>(p) >> 4) + elem_offset) & 7u);
 }
 
-template <class TagT, int LAYOUT, bool RESID, bool BASE_AL, int OWN>
+template <class TagT, int LAYOUT, bool RESID, bool BASE_AL>
 __global__ __launch_bounds__(kBlock) void k_project_al(acm_camera cam, size_t n,
                                                        const double* __restrict__ pts,
                                                        const double* __restrict__ obs,
                                                        int policy, double* __restrict__ out2,
                                                        uint8_t* __restrict__ status,
                                                        double* __restrict__ jac) {
-    static_assert(OWN == kBlock || OWN == kBlock - kAlLead, "OWN");
     using M = typename TagT::template type<double>;
     constexpr int P = M::P;
     constexpr int D = P - 4;
-    constexpr int S = OWN + kAlLead;          // LDS slots: own points, then the lead-in
+    constexpr int S = kAlOwn + kAlLead;          // LDS slots: own points, then the lead-in
     constexpr int NW = BASE_AL ? 1 : S;       // s_uv / s_a only when they can be shifted
     __shared__ double2 s_uv[NW];
     __shared__ double s_a[NW];
@@ -282,9 +304,11 @@ __global__ __launch_bounds__(kBlock) void k_project_al(acm_camera cam, size_t n,
     __shared__ uint8_t s_ok[S];
     const Cam<double> c = make_cam<double>(cam);
     const int t = threadIdx.x;
-    const size_t base = (size_t)blockIdx.x * OWN;
+    const size_t base = (size_t)blockIdx.x * kAlOwn;
     auto eval = [&](size_t p, bool have, int slot, bool own) {
         double x = 0.0, y = 0.0, z = 1.0;
+        // plain loads: non-temporal ones measured 25% slower here (the
+        // lead-in re-read and the nt store stream, profiles/r01_ne_sweep.log)
         if (have) load_point<LAYOUT>(pts, n, p, x, y, z);
         double u, v, ju[P], jv[P];
         const uint8_t st = M::template project<true>(c, x, y, z, u, v, ju, jv);
@@ -292,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void k_project_al(acm_camera cam, size_t n,
         double2 w;
         if (RESID) {
             double2 o = make_double2(0.0, 0.0);
-            if (have) o = *reinterpret_cast<const double2*>(obs + 2 * p);
+            if (have) o = ld2<false>(obs + 2 * p);
             const double sent = policy == ACM_INVALID_SENTINEL ? 1e6 : 0.0;
             w = make_double2(ok ? u - o.x : sent, ok ? v - o.y : sent);
         } else {
@@ -315,17 +339,10 @@ __global__ __launch_bounds__(kBlock) void k_project_al(acm_camera cam, size_t n,
             s_d[k][slot] = make_double2(ok ? ju[4 + k] : 0.0, ok ? jv[4 + k] : 0.0);
         if (status && own && have) st1<true>(status + p, st);
     };
-    // lead-in point k (0..7) = base - 8 + k, in slot OWN + k
-    if (OWN == kBlock) {
-        eval(base + t, base + t < n, t, true);
-        if (t < kAlLead) eval(base + t - kAlLead, base >= (size_t)kAlLead, OWN + t, false);
-    } else if (t < OWN) {
-        eval(base + t, base + t < n, t, true);
-    } else {
-        eval(base + t - kBlock, base >= (size_t)kAlLead, t, false);
-    }
+    // lead-in point k (0..7) = base - 8 + k, in slot kAlOwn + k
+    eval(base + t, base + t < n, t, true);
+    if (t < kAlLead) eval(base + t - kAlLead, base >= (size_t)kAlLead, kAlOwn + t, false);
     __syncthreads();
-    if (t >= OWN) return;
     // element base - sh + t of a stream sitting sh elements off the line grid:
     // own point base + t - sh (slot t - sh) or lead-in slot S - sh + t
     size_t e;
@@ -355,22 +372,17 @@ static bool al_base_aligned(const void* out2, const double* jac) {
            (reinterpret_cast<uintptr_t>(jac) & 127u) == 0;
 }
 
-// workgroups so that the last window [B*OWN - s, ...) reaches n for every s <= 7
-static unsigned al_blocks(size_t n, int own) { return (unsigned)((n + kAlLead - 1 + own) / own); }
+// workgroups so that the last window [B*kAlOwn - s, ...) reaches n for every s <= 7
+static unsigned al_blocks(size_t n) { return (unsigned)((n + kAlLead - 1 + kAlOwn) / kAlOwn); }
 
-// g_align_j: 2 forces the OWN = 248 variant (A/B), anything else uses 256.
 template <class TagT, int LAY, bool RESID>
 static void launch_al(hipStream_t s, const acm_camera& cam, size_t n, const double* pts,
                       const double* obs, int policy, double* out2, uint8_t* status,
                       double* jac) {
-    const bool bal = al_base_aligned(out2, jac);
-    const int own = g_align_j == 2 ? kBlock - kAlLead : kBlock;
-    auto kern = bal ? (own == kBlock ? k_project_al<TagT, LAY, RESID, true, kBlock>
-                                     : k_project_al<TagT, LAY, RESID, true, kBlock - kAlLead>)
-                    : (own == kBlock ? k_project_al<TagT, LAY, RESID, false, kBlock>
-                                     : k_project_al<TagT, LAY, RESID, false, kBlock - kAlLead>);
-    hipLaunchKernelGGL(kern, dim3(al_blocks(n, own)), dim3(kBlock), 0, s, cam, n, pts, obs,
-                       policy, out2, status, jac);
+    auto kern = al_base_aligned(out2, jac) ? k_project_al<TagT, LAY, RESID, true>
+                                           : k_project_al<TagT, LAY, RESID, false>;
+    hipLaunchKernelGGL(kern, dim3(al_blocks(n)), dim3(kBlock), 0, s, cam, n, pts, obs, policy,
+                       out2, status, jac);
 }
 
 // --------------------------------------------------------------- unproject
@@ -505,14 +517,12 @@ struct NE {
 };
 
 // Per-model (waves, points per lane step) of k_normal_eq: the fastest cell of
-// the interleaved {1,3,4} x {1,2,4} sweep (tools/bench_configs.py --configs
-// 3ne, profiles/r01_ne_sweep.log, 10M points).  All cells give the same sums
-// up to summation order.
+// the interleaved {1,3,4} x {1,2} x nt-loads sweep (tools/bench_configs.py
+// --configs 3ne, profiles/r01_ne_sweep.log, 10M points).  All cells give the
+// same sums up to summation order.
 template <class TagT> struct NeDefault { static constexpr int W = 3, U = 1; };
-template <> struct NeDefault<Tag<Pinhole>> { static constexpr int W = 3, U = 4; };
-template <> struct NeDefault<Tag<RadTan>> { static constexpr int W = 1, U = 2; };
-template <> struct NeDefault<Tag<DoubleSphere>> { static constexpr int W = 4, U = 2; };
-template <> struct NeDefault<Tag<Eucm>> { static constexpr int W = 4, U = 2; };
+template <> struct NeDefault<Tag<RadTan>> { static constexpr int W = 3, U = 2; };
+template <> struct NeDefault<Tag<Fov>> { static constexpr int W = 4, U = 1; };
 
 constexpr int kNeMaxBlocks = 2048;  // reprojection stats / median partials
 constexpr int kNqMaxBlocks = 2048;  // normal equations: 8 workgroups per CU
@@ -561,7 +571,7 @@ static int resident_blocks(const void* kernel) {
 // (amdgpu_waves_per_eu).  1 leaves it free (KB lands at 176 VGPRs = 2 waves);
 // 3 fits KB in 168 without spills; 4 forces 128 with scratch spills for KB and
 // RadTan.  Selected per launch by ACM_TUNE_NE_WAVES (results identical).
-template <class TagT, int LAYOUT, int WAVES, int U>
+template <class TagT, int LAYOUT, int WAVES, int U, bool NTL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq(acm_camera cam, size_t n,
                                                       const double* __restrict__ pts,
                                                       const double* __restrict__ obs, int policy,
@@ -622,8 +632,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         double x = 0, y = 0, z = 1;
         double2 o = make_double2(0.0, 0.0);
         if (kPrefetch && i < n) {
-            load_point<LAYOUT>(pts, n, i, x, y, z);
-            o = *reinterpret_cast<const double2*>(obs + 2 * i);
+            load_point<LAYOUT, NTL>(pts, n, i, x, y, z);
+            o = ld2<NTL>(obs + 2 * i);
         }
         for (; i < n; i += stride) {
             const size_t inext = i + stride;
@@ -631,12 +641,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             double2 on = make_double2(0.0, 0.0);
             if (kPrefetch) {
                 if (inext < n) {
-                    load_point<LAYOUT>(pts, n, inext, xn, yn, zn);
-                    on = *reinterpret_cast<const double2*>(obs + 2 * inext);
+                    load_point<LAYOUT, NTL>(pts, n, inext, xn, yn, zn);
+                    on = ld2<NTL>(obs + 2 * inext);
                 }
             } else {
-                load_point<LAYOUT>(pts, n, i, x, y, z);
-                o = *reinterpret_cast<const double2*>(obs + 2 * i);
+                load_point<LAYOUT, NTL>(pts, n, i, x, y, z);
+                o = ld2<NTL>(obs + 2 * i);
             }
             accumulate(x, y, z, o);
             if (kPrefetch) { x = xn; y = yn; z = zn; o = on; }
@@ -652,8 +662,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                 xs[u] = 0.0; ys[u] = 0.0; zs[u] = 1.0;
                 os[u] = make_double2(0.0, 0.0);
                 if (j < n) {
-                    load_point<LAYOUT>(pts, n, j, xs[u], ys[u], zs[u]);
-                    os[u] = *reinterpret_cast<const double2*>(obs + 2 * j);
+                    load_point<LAYOUT, NTL>(pts, n, j, xs[u], ys[u], zs[u]);
+                    os[u] = ld2<NTL>(obs + 2 * j);
                 }
             }
         };
@@ -1653,9 +1663,9 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
         const int un = g_ne_unroll ? g_ne_unroll : Def::U;
         auto go = [&](auto lay_c, auto w_c) {
             constexpr int LAY = decltype(lay_c)::value, W = decltype(w_c)::value;
-            auto kern = k_normal_eq<TagT, LAY, W, 1>;
-            if (un == 2) kern = k_normal_eq<TagT, LAY, W, 2>;
-            if (un == 4) kern = k_normal_eq<TagT, LAY, W, 4>;
+            const bool ntl = g_nt_loads != 0;
+            auto kern = ntl ? k_normal_eq<TagT, LAY, W, 1, true> : k_normal_eq<TagT, LAY, W, 1, false>;
+            if (un == 2) kern = ntl ? k_normal_eq<TagT, LAY, W, 2, true> : k_normal_eq<TagT, LAY, W, 2, false>;
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
@@ -2039,16 +2049,22 @@ ACM_API int acm_set_tuning(int key, int value) {
         return old;
     }
     if (key == ACM_TUNE_NE_UNROLL) {
-        if (value != 0 && value != 1 && value != 2 && value != 4)
-            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 0 (per-model default), 1, 2 or 4");
+        if (value != 0 && value != 1 && value != 2)
+            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 0 (per-model default), 1 or 2");
         const int old = g_ne_unroll;
         g_ne_unroll = value;
         return old;
     }
     if (key == ACM_TUNE_ALIGN_J) {
-        if (value < -1 || value > 2) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..2");
+        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
         const int old = g_align_j;
         g_align_j = value;
+        return old;
+    }
+    if (key == ACM_TUNE_NT_LOADS) {
+        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
+        const int old = g_nt_loads;
+        g_nt_loads = value;
         return old;
     }
     if (key == ACM_TUNE_FOV_UNROLL) {

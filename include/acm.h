@@ -361,19 +361,21 @@ ACM_API int acm_stream_synchronize(void *stream);
  * minimum waves per SIMD the normal-equations kernel is compiled for
  * (0 = per-model default, 1, 3, 4).  ACM_TUNE_FOV_UNROLL: points per lane step of the FOV
  * grid search (1, 2 = default, 4).  ACM_TUNE_NE_UNROLL: points per lane step
- * of the normal-equations kernel (0 = per-model default, 1, 2, 4).
+ * of the normal-equations kernel (0 = per-model default, 1, 2).
  * ACM_TUNE_ALIGN_J: kernel of +Jacobian launches of acm_project /
  * acm_residual_jacobian: -1 = auto (default) = line-aligned store windows
- * through LDS, 0 = one point per lane with direct stores, 1 = aligned,
- * 2 = aligned with 248-point workgroup windows (A/B only).  Returns the
- * previous value or an error. */
+ * through LDS, 0 = one point per lane with direct stores, 1 = aligned.
+ * ACM_TUNE_NT_LOADS: non-temporal loads of the point / observation streams
+ * in the normal-equations kernel (-1 = auto = on, 0, 1).
+ * Returns the previous value or an error. */
 enum {
     ACM_TUNE_PROJECT_VARIANT = 0,
     ACM_TUNE_RESIDUAL_NT = 1,
     ACM_TUNE_NE_WAVES = 2,
     ACM_TUNE_FOV_UNROLL = 3,
     ACM_TUNE_NE_UNROLL = 4,
-    ACM_TUNE_ALIGN_J = 5
+    ACM_TUNE_ALIGN_J = 5,
+    ACM_TUNE_NT_LOADS = 6
 };
 ACM_API int acm_set_tuning(int key, int value);
 

@@ -40,19 +40,29 @@ def _guarded(torch, n_f64, off):
     return buf, start
 
 
+def _set_align(_lib, L, align):
+    """align 0 = direct kernel, 1 = line-aligned kernel, -1 = library
+    default; returns an undo callable"""
+    oa = L.acm_set_tuning(_lib.TUNE_ALIGN_J, align)
+
+    def undo():
+        L.acm_set_tuning(_lib.TUNE_ALIGN_J, oa)
+    return undo
+
+
 def _run_project(torch, _lib, L, cam, pts, P, layout, align, off_uv=0, off_j=0):
     n = pts.shape[0] if layout == 0 else pts.shape[1]
     uvb, su = _guarded(torch, 2 * n, off_uv)
     jb, sj = _guarded(torch, 2 * n * P, off_j)
     stb = torch.full((n + 2 * GUARD,), 0xAB, dtype=torch.uint8, device="cuda")
-    old = L.acm_set_tuning(_lib.TUNE_ALIGN_J, align)
+    undo = _set_align(_lib, L, align)
     try:
         _lib.check(L.acm_project(ctypes.byref(cam), n, pts.data_ptr(), layout,
                                  uvb.data_ptr() + 8 * su, stb.data_ptr() + GUARD,
                                  jb.data_ptr() + 8 * sj, None))
         torch.cuda.synchronize()
     finally:
-        L.acm_set_tuning(_lib.TUNE_ALIGN_J, old)
+        undo()
     uvb, jb, stb = uvb.cpu(), jb.cpu(), stb.cpu()
     assert torch.all(uvb[:su] == 7.25) and torch.all(uvb[su + 2 * n:] == 7.25), "uv guard"
     assert torch.all(jb[:sj] == 7.25) and torch.all(jb[sj + 2 * n * P:] == 7.25), "J guard"
@@ -70,7 +80,7 @@ def test_aligned_project_bit_identical(model):
         for layout in (0, 1):
             pts = torch.as_tensor(pts_np if layout == 0 else pts_np.T.copy(), device="cuda")
             a = _run_project(torch, _lib, L, cam, pts, P, layout, 0)
-            for al in (1, 2):
+            for al in (1, -1):
                 b = _run_project(torch, _lib, L, cam, pts, P, layout, al)
                 for x, y, name in zip(a, b, ("uv", "status", "J")):
                     assert torch.equal(x.view(torch.int64) if x.dtype == torch.float64 else x,
@@ -90,7 +100,7 @@ def test_aligned_project_buffer_offsets(model, offs):
     n = 10_007
     pts = torch.as_tensor(samples.synthetic_points(n), device="cuda")
     ref = _run_project(torch, _lib, L, cam, pts, P, 0, 0)
-    for align in (-1, 1, 2):
+    for align in (-1, 1):
         got = _run_project(torch, _lib, L, cam, pts, P, 0, align, off_uv=offs[0], off_j=offs[1])
         for x, y in zip(ref, got):
             assert torch.equal(x, y) if x.dtype == torch.uint8 else \
@@ -109,12 +119,12 @@ def test_aligned_residual_bit_identical(model, policy):
         obs = torch.as_tensor(np.where(np.isnan(uv0), 3.0, uv0) + 0.25, device="cuda")
         pts = torch.as_tensor(pts_np, device="cuda")
         outs = []
-        for align in (0, 1, 2):
+        for align in (0, 1):
             for with_status in (True, False):
                 rb, sr = _guarded(torch, 2 * n, 0)
                 jb, sj = _guarded(torch, 2 * n * P, 0)
                 stb = torch.full((n + 2 * GUARD,), 0xAB, dtype=torch.uint8, device="cuda")
-                old = L.acm_set_tuning(_lib.TUNE_ALIGN_J, align)
+                undo = _set_align(_lib, L, align)
                 try:
                     _lib.check(L.acm_residual_jacobian(
                         ctypes.byref(cam), n, pts.data_ptr(), 0, obs.data_ptr(), policy,
@@ -122,7 +132,7 @@ def test_aligned_residual_bit_identical(model, policy):
                         stb.data_ptr() + GUARD if with_status else None, None))
                     torch.cuda.synchronize()
                 finally:
-                    L.acm_set_tuning(_lib.TUNE_ALIGN_J, old)
+                    undo()
                 rb, jb, stb = rb.cpu(), jb.cpu(), stb.cpu()
                 assert torch.all(rb[:sr] == 7.25) and torch.all(rb[sr + 2 * n:] == 7.25)
                 assert torch.all(jb[:sj] == 7.25) and torch.all(jb[sj + 2 * n * P:] == 7.25)

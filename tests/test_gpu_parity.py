@@ -184,18 +184,22 @@ def test_normal_equations_every_tuning_cell(model):
     L = _lib.load()
     try:
         for wv in (0, 1, 3, 4):
-            for un in (0, 1, 2, 4):
-                L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)
-                L.acm_set_tuning(_lib.TUNE_NE_UNROLL, un)
-                res = f.normal_equations(params)
-                A, b, c, nv = [t.cpu().numpy() for t in f.unpack_normal_equations(res, P)]
-                assert int(nv) == nv0, (wv, un)
-                assert np.abs(A - A0).max() <= TOL * np.abs(A0).max(), (wv, un)
-                assert np.abs(b - b0).max() <= TOL * max(np.abs(b0).max(), 1.0), (wv, un)
-                assert abs(c - c0) <= TOL * max(abs(c0), 1.0), (wv, un)
+            for un in (0, 1, 2):
+                for ntl in (-1, 0):
+                    L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)
+                    L.acm_set_tuning(_lib.TUNE_NE_UNROLL, un)
+                    L.acm_set_tuning(_lib.TUNE_NT_LOADS, ntl)
+                    cell = (wv, un, ntl)
+                    res = f.normal_equations(params)
+                    A, b, c, nv = [t.cpu().numpy() for t in f.unpack_normal_equations(res, P)]
+                    assert int(nv) == nv0, cell
+                    assert np.abs(A - A0).max() <= TOL * np.abs(A0).max(), cell
+                    assert np.abs(b - b0).max() <= TOL * max(np.abs(b0).max(), 1.0), cell
+                    assert abs(c - c0) <= TOL * max(abs(c0), 1.0), cell
     finally:
         L.acm_set_tuning(_lib.TUNE_NE_WAVES, 0)
         L.acm_set_tuning(_lib.TUNE_NE_UNROLL, 0)
+        L.acm_set_tuning(_lib.TUNE_NT_LOADS, -1)
 
 
 @pytest.mark.parametrize("model", range(7))

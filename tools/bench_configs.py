@@ -135,25 +135,28 @@ def config3_ne_all(n):
         out = torch.empty((P * P + P + 2,), dtype=torch.float64, device="cuda")
         L = _lib.load()
         res = {}
-        combos = [(0, 0)] + [(wv, un) for wv in (1, 3, 4) for un in (1, 2, 4)]
-        for rep in range(2):  # interleaved A/B of register target x points per lane step
-            for wv, un in combos:
+        combos = [(0, 0, -1)] + [(wv, un, nl) for wv in (1, 3, 4) for un in (1, 2)
+                                 for nl in (0, 1)]
+        for rep in range(2):  # interleaved A/B: register target x lane step x nt loads
+            for wv, un, nl in combos:
                 L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)
                 L.acm_set_tuning(_lib.TUNE_NE_UNROLL, un)
-                res.setdefault((wv, un), []).append(
+                L.acm_set_tuning(_lib.TUNE_NT_LOADS, nl)
+                res.setdefault((wv, un, nl), []).append(
                     timed(lambda: f.normal_equations(params, out)))
-                if rep == 0 and (wv, un) == combos[0]:
+                if rep == 0 and (wv, un, nl) == combos[0]:
                     ref = out.clone()
                 elif rep == 0:  # grid size / lane order -> summation order
                     assert torch.allclose(out, ref, rtol=1e-12, atol=0.0)
         L.acm_set_tuning(_lib.TUNE_NE_WAVES, 0)
         L.acm_set_tuning(_lib.TUNE_NE_UNROLL, 0)
+        L.acm_set_tuning(_lib.TUNE_NT_LOADS, -1)
         ms = {k: min(v) for k, v in res.items()}
         best = min(ms, key=ms.get)
         emit({"config": 3, "what": "fused normal equations", "model": fcls.MODEL.__name__,
-              "points": n, "ms_by_waves_unroll": {f"w{k[0]}u{k[1]}": round(v, 4)
-                                                  for k, v in ms.items()},
-              "best": f"w{best[0]}u{best[1]}", "Mpoints_per_s": round(n / ms[best] / 1e3, 1),
+              "points": n, "ms_by_waves_unroll_ntl": {f"w{k[0]}u{k[1]}n{k[2]}": round(v, 4)
+                                                      for k, v in ms.items()},
+              "best": f"w{best[0]}u{best[1]}n{best[2]}", "Mpoints_per_s": round(n / ms[best] / 1e3, 1),
               "GBps": round(40 * n / ms[best] / 1e6, 1)})
 
 

@@ -61,8 +61,7 @@ def main():
                         L.acm_project(ctypes.byref(cam), n, pts.data_ptr(), 0, uv.data_ptr(),
                                       st.data_ptr(), jac.data_ptr(), sh)
                     return f
-                for k, f in (("mimic", mim), ("kb", real(0)), ("kbaligned", real(1)),
-                             ("kbaligned248", real(2))):
+                for k, f in (("mimic", mim), ("kb", real(0)), ("kbaligned", real(1))):
                     key = f"{k}_n{n}_{'nt' if nt else 'plain'}"
                     ms = timed(f)
                     out[key] = min(out.get(key, 1e9), ms)

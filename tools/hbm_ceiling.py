@@ -28,7 +28,7 @@ def main():
     import torch
     L = ctypes.CDLL(LIB)
     vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
-    L.acm_probe_read.argtypes = [vp, sz, vp, ci, vp]
+    L.acm_probe_read.argtypes = [vp, sz, vp, ci, ci, ci, vp]
     L.acm_probe_write.argtypes = [vp, sz, ci, vp]
     L.acm_probe_mimic.argtypes = [sz, vp, vp, vp, vp, ci, ci, vp]
     sh = torch.cuda.current_stream().cuda_stream
@@ -55,12 +55,17 @@ def main():
         out[key] = {"ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1),
                     "bytes": nbytes}
 
-    acc = torch.zeros((cus * 16 * 4,), dtype=torch.float64, device="cuda")  # wave partials
+    acc = torch.zeros((cus * 32 * 4,), dtype=torch.float64, device="cuda")  # wave partials
     for nb in (40 * n, 160 * n):  # NE's 40 B/pt stream; a 4x larger one
         buf = torch.empty((nb // 8,), dtype=torch.float64, device="cuda").fill_(1.0)
-        for g in (cus * 8, cus * 16):
-            cell(f"read_{nb >> 20}MiB_grid{g}",
-                 lambda: L.acm_probe_read(buf.data_ptr(), nb, acc.data_ptr(), g, sh), nb)
+        for g in (cus * 4, cus * 8, cus * 16, cus * 32):
+            for un in (1, 2, 4, 8):
+                for nt in (0, 1):
+                    if nb > 40 * n and (un != 2 or g != cus * 8):
+                        continue
+                    cell(f"read_{nb >> 20}MiB_grid{g}_u{un}{'_nt' if nt else ''}",
+                         lambda: L.acm_probe_read(buf.data_ptr(), nb, acc.data_ptr(), g, un, nt,
+                                                  sh), nb)
         del buf
     wb = 169 * n
     buf = torch.empty((wb // 8,), dtype=torch.float64, device="cuda")

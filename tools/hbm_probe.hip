@@ -25,17 +25,23 @@ __device__ __forceinline__ void put2(double* p, double a, double b) {
     else *reinterpret_cast<dbl2*>(p) = v;
 }
 
+// U independent 16-B loads in flight per lane per step; NT = non-temporal loads
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_read(const dbl2* __restrict__ p, size_t n2,
                                               double* __restrict__ out) {
     // one partial per wave (no same-address atomics: they would serialise)
     double s = 0.0;
     const size_t stride = (size_t)gridDim.x * 256;
     size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    for (; i + stride < n2; i += 2 * stride) {
-        const dbl2 a = p[i], b = p[i + stride];
-        s += a.x + a.y + b.x + b.y;
+    for (; i + (U - 1) * stride < n2; i += U * stride) {
+        dbl2 a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            a[u] = NT ? __builtin_nontemporal_load(p + i + u * stride) : p[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) s += a[u].x + a[u].y;
     }
-    if (i < n2) { const dbl2 a = p[i]; s += a.x + a.y; }
+    for (; i < n2; i += stride) { const dbl2 a = p[i]; s += a.x + a.y; }
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
     if ((threadIdx.x & 63) == 0) out[(size_t)blockIdx.x * 4 + (threadIdx.x >> 6)] = s;
 }
@@ -64,11 +70,21 @@ static unsigned blocks(size_t n) { return (unsigned)((n + 255) / 256); }
 
 extern "C" {
 
-int acm_probe_read(const void* buf, size_t bytes, double* out, int grid, void* stream) {
+int acm_probe_read(const void* buf, size_t bytes, double* out, int grid, int unroll, int nt,
+                   void* stream) {
     const size_t n2 = bytes / 16;
-    hipLaunchKernelGGL(k_read, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       (const dbl2*)buf, n2, out);
-    return (int)hipGetLastError();
+    hipStream_t s = (hipStream_t)stream;
+#define RD(U)                                                                                   \
+    if (unroll == U) {                                                                          \
+        if (nt) hipLaunchKernelGGL((k_read<U, true>), dim3(grid), dim3(256), 0, s, (const dbl2*)buf, \
+                                   n2, out);                                                    \
+        else hipLaunchKernelGGL((k_read<U, false>), dim3(grid), dim3(256), 0, s, (const dbl2*)buf, \
+                                n2, out);                                                       \
+        return (int)hipGetLastError();                                                          \
+    }
+    RD(1) RD(2) RD(4) RD(8)
+#undef RD
+    return -1;
 }
 
 int acm_probe_write(void* buf, size_t bytes, int nt, void* stream) {
