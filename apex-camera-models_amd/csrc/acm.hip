@@ -522,6 +522,8 @@ struct NE {
 // same sums up to summation order.
 template <class TagT> struct NeDefault { static constexpr int W = 3, U = 1; };
 template <> struct NeDefault<Tag<RadTan>> { static constexpr int W = 3, U = 2; };
+template <> struct NeDefault<Tag<Ucm>> { static constexpr int W = 3, U = 2; };
+template <> struct NeDefault<Tag<Eucm>> { static constexpr int W = 3, U = 2; };
 template <> struct NeDefault<Tag<Fov>> { static constexpr int W = 4, U = 1; };
 
 constexpr int kNeMaxBlocks = 2048;  // reprojection stats / median partials
@@ -593,20 +595,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // ACM_TUNE_NE_UNROLL).  Not for the largest accumulator sets (KB,
     // RadTan), where the extra registers cost a wave of occupancy.
     constexpr bool kPrefetch = K <= 40;
+    // FAST projection (reciprocal instead of per-point divisions) and fused
+    // multiply-adds: the sums are held to 1e-10, not to the reference's
+    // operation order, and the validity mask stays exact (camera_models.hpp).
     auto accumulate = [&](double px, double py, double pz, double2 po) {
         double u, v, ju[P], jv[P];
-        const uint8_t st = M::template project<true>(c, px, py, pz, u, v, ju, jv);
+        const uint8_t st = M::template project<true, true>(c, px, py, pz, u, v, ju, jv);
         if (st == ST_OK) {
             const double r0 = u - po.x, r1 = v - po.y;
             const double a = ju[0], b = jv[1];
-            acc[0] += a * a;
+            acc[0] = fma(a, a, acc[0]);
             acc[1] += a;
-            acc[L::B2] += b * b;
+            acc[L::B2] = fma(b, b, acc[L::B2]);
             acc[L::B1] += b;
 #pragma unroll
             for (int k = 0; k < D; ++k) {
-                acc[L::A_DU + k] += a * ju[4 + k];
-                acc[L::B_DV + k] += b * jv[4 + k];
+                acc[L::A_DU + k] = fma(a, ju[4 + k], acc[L::A_DU + k]);
+                acc[L::B_DV + k] = fma(b, jv[4 + k], acc[L::B_DV + k]);
                 acc[L::DU + k] += ju[4 + k];
                 acc[L::DV + k] += jv[4 + k];
             }
@@ -614,15 +619,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
 #pragma unroll
             for (int j = 0; j < D; ++j) {
 #pragma unroll
-                for (int k = j; k < D; ++k) acc[t++] += ju[4 + j] * ju[4 + k] + jv[4 + j] * jv[4 + k];
+                for (int k = j; k < D; ++k, ++t)
+                    acc[t] = fma(ju[4 + j], ju[4 + k], fma(jv[4 + j], jv[4 + k], acc[t]));
             }
-            acc[L::G + 0] += a * r0;
-            acc[L::G + 1] += b * r1;
+            acc[L::G + 0] = fma(a, r0, acc[L::G + 0]);
+            acc[L::G + 1] = fma(b, r1, acc[L::G + 1]);
             acc[L::G + 2] += r0;
             acc[L::G + 3] += r1;
 #pragma unroll
-            for (int k = 0; k < D; ++k) acc[L::G + 4 + k] += ju[4 + k] * r0 + jv[4 + k] * r1;
-            acc[K - 2] += r0 * r0 + r1 * r1;
+            for (int k = 0; k < D; ++k)
+                acc[L::G + 4 + k] = fma(ju[4 + k], r0, fma(jv[4 + k], r1, acc[L::G + 4 + k]));
+            acc[K - 2] = fma(r0, r0, fma(r1, r1, acc[K - 2]));
             acc[K - 1] += 1.0;
         } else {
             acc[K - 2] += sent2;

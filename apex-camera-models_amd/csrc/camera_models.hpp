@@ -14,6 +14,14 @@
 // Status decisions are computed branch-free where possible so a wave does
 // not diverge on the rare failing point; the caller selects outputs.
 //
+// project<WJ, FAST>: FAST = true (used only by the fused normal-equations
+// kernel, whose sums are held to 1e-10 anyway and are summed in a different
+// order than the reference) replaces the divisions by a per-point denominator
+// with one reciprocal and multiplies: u, v, J within ~1 ulp of the exact
+// path.  Status decisions never depend on those divisions, so the validity
+// mask (and n_valid) stays bit-exact.  Every other caller uses FAST = false,
+// the reference's operation order.
+//
 // Reference citations: /root/reference/src/camera/<model>.rs:line.
 #pragma once
 
@@ -60,18 +68,19 @@ template <class T>
 struct Pinhole {
     static constexpr int P = 4;
     // pinhole.rs:165-182
-    template <bool WJ>
+    template <bool WJ, bool FAST = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
-        u = fx * x / z + cx;  // :170
-        v = fy * y / z + cy;  // :171
+        const T iz = FAST ? T(1) / z : T(0);
+        u = FAST ? fx * (x * iz) + cx : fx * x / z + cx;  // :170
+        v = FAST ? fy * (y * iz) + cy : fy * y / z + cy;  // :171
         uint8_t st = ST_OK;
         if (u < T(0) || u >= c.w || v < T(0) || v >= c.h) st = ST_PROJECTION_OUT_SIDE_IMAGE;
         if (z < T(kEpsSqrt)) st = ST_POINT_AT_CAMERA_CENTER;  // :167, checked first
         if (WJ) {
-            ju[0] = x / z; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
-            jv[0] = T(0); jv[1] = y / z; jv[2] = T(0); jv[3] = T(1);
+            ju[0] = FAST ? x * iz : x / z; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
+            jv[0] = T(0); jv[1] = FAST ? y * iz : y / z; jv[2] = T(0); jv[3] = T(1);
         }
         return st;
     }
@@ -97,12 +106,13 @@ template <class T>
 struct RadTan {
     static constexpr int P = 9;  // fx fy cx cy k1 k2 p1 p2 k3
     // rad_tan.rs:302-348
-    template <bool WJ>
+    template <bool WJ, bool FAST = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
         const T k1 = c.p[4], k2 = c.p[5], p1 = c.p[6], p2 = c.p[7], k3 = c.p[8];
-        T xp = x / z, yp = y / z;
+        const T iz = FAST ? T(1) / z : T(0);
+        T xp = FAST ? x * iz : x / z, yp = FAST ? y * iz : y / z;
         T r2 = xp * xp + yp * yp;
         T r4 = r2 * r2;
         T r6 = r4 * r2;
@@ -192,7 +202,7 @@ template <class T>
 struct KannalaBrandt {
     static constexpr int P = 8;  // fx fy cx cy k1 k2 k3 k4
     // kannala_brandt.rs:340-394
-    template <bool WJ>
+    template <bool WJ, bool FAST = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
@@ -208,8 +218,9 @@ struct KannalaBrandt {
         T theta9 = theta7 * theta2;
         T theta_d = theta + k1 * theta3 + k2 * theta5 + k3 * theta7 + k4 * theta9;
         const bool axis = r < T(kEps);  // :375
-        T x_r = axis ? T(0) : x / r;
-        T y_r = axis ? T(0) : y / r;
+        const T ir = FAST ? T(1) / r : T(0);
+        T x_r = axis ? T(0) : (FAST ? x * ir : x / r);
+        T y_r = axis ? T(0) : (FAST ? y * ir : y / r);
         u = fx * theta_d * x_r + cx;  // :390
         v = fy * theta_d * y_r + cy;
         if (WJ) {
@@ -275,7 +286,7 @@ template <class T>
 struct DoubleSphere {
     static constexpr int P = 6;  // fx fy cx cy alpha xi
     // double_sphere.rs:361-390 + check_projection_condition :177-184
-    template <bool WJ>
+    template <bool WJ, bool FAST = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
@@ -289,11 +300,12 @@ struct DoubleSphere {
         T w1 = alpha <= T(0.5) ? alpha / (T(1) - alpha) : (T(1) - alpha) / alpha;
         T w2 = (w1 + xi) / sqrt(T(2) * w1 * xi + xi * xi + T(1));
         const bool ok = !(denom < T(1e-3)) && (z > -w2 * d1);
-        T mx = x / denom, my = y / denom;
+        const T id = FAST ? T(1) / denom : T(0);
+        T mx = FAST ? x * id : x / denom, my = FAST ? y * id : y / denom;
         u = fx * (mx) + cx;
         v = fy * (my) + cy;
         if (WJ) {
-            T tu = fx * mx / denom, tv = fy * my / denom;
+            T tu = FAST ? fx * mx * id : fx * mx / denom, tv = FAST ? fy * my * id : fy * my / denom;
             T dda = d2 - gamma;
             T ddx = d1 * (alpha * gamma / d2 + (T(1) - alpha));
             ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
@@ -334,7 +346,7 @@ template <class T>
 struct Ucm {
     static constexpr int P = 5;  // fx fy cx cy alpha
     // ucm.rs:297-316 + check_proj_condition :154-161
-    template <bool WJ>
+    template <bool WJ, bool FAST = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], alpha = c.p[4];
@@ -342,11 +354,12 @@ struct Ucm {
         T denom = alpha * d + (T(1) - alpha) * z;
         T w = alpha <= T(0.5) ? alpha / (T(1) - alpha) : (T(1) - alpha) / alpha;
         const bool ok = !(denom < T(1e-3)) && (z > -w * d);
-        T mx = x / denom, my = y / denom;
+        const T id = FAST ? T(1) / denom : T(0);
+        T mx = FAST ? x * id : x / denom, my = FAST ? y * id : y / denom;
         u = fx * mx + cx;
         v = fy * my + cy;
         if (WJ) {
-            T tu = fx * mx / denom, tv = fy * my / denom;
+            T tu = FAST ? fx * mx * id : fx * mx / denom, tv = FAST ? fy * my * id : fy * my / denom;
             T dda = d - z;
             ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0); ju[4] = -tu * dda;
             jv[0] = T(0); jv[1] = my; jv[2] = T(0); jv[3] = T(1); jv[4] = -tv * dda;
@@ -381,7 +394,7 @@ template <class T>
 struct Eucm {
     static constexpr int P = 6;  // fx fy cx cy alpha beta
     // eucm.rs:328-347 + check_proj_condition :167-177
-    template <bool WJ>
+    template <bool WJ, bool FAST = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
@@ -395,11 +408,12 @@ struct Eucm {
             cond = !(z < denom * cc);
         }
         const bool ok = !(denom < T(1e-3)) && cond;
-        T mx = x / denom, my = y / denom;
+        const T id = FAST ? T(1) / denom : T(0);
+        T mx = FAST ? x * id : x / denom, my = FAST ? y * id : y / denom;
         u = fx * mx + cx;
         v = fy * my + cy;
         if (WJ) {
-            T tu = fx * mx / denom, tv = fy * my / denom;
+            T tu = FAST ? fx * mx * id : fx * mx / denom, tv = FAST ? fy * my * id : fy * my / denom;
             T dda = d - z;
             T ddb = alpha * rr / (T(2) * d);
             ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
@@ -436,7 +450,7 @@ template <class T>
 struct Fov {
     static constexpr int P = 5;  // fx fy cx cy w
     // fov.rs:284-316
-    template <bool WJ>
+    template <bool WJ, bool FAST = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], wf = c.p[4];
@@ -445,7 +459,8 @@ struct Fov {
         const T tan_w_half = c.p[8];  // tan(w / 2), host-precomputed (acm.hip prep)
         T atan_wrd = atan2(T(2) * tan_w_half * r, z);
         const bool axis = r2 < T(kEpsSqrt);
-        T rd = axis ? T(2) * tan_w_half / wf : atan_wrd / (r * wf);
+        const T irw = FAST ? T(1) / (r * wf) : T(0);
+        T rd = axis ? T(2) * tan_w_half / wf : (FAST ? atan_wrd * irw : atan_wrd / (r * wf));
         T mx = x * rd, my = y * rd;
         u = fx * mx + cx;
         v = fy * my + cy;
@@ -456,7 +471,8 @@ struct Fov {
             } else {
                 T a = T(2) * tan_w_half * r;
                 T datan = z * r * (T(1) + tan_w_half * tan_w_half) / (a * a + z * z);
-                drd = datan / (r * wf) - atan_wrd / (r * wf * wf);
+                drd = FAST ? datan * irw - atan_wrd * irw / wf
+                           : datan / (r * wf) - atan_wrd / (r * wf * wf);
             }
             ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0); ju[4] = fx * x * drd;
             jv[0] = T(0); jv[1] = my; jv[2] = T(0); jv[3] = T(1); jv[4] = fy * y * drd;

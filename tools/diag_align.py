@@ -23,7 +23,7 @@ def main():
     L = _lib.load()
     Pr = ctypes.CDLL(os.path.join(HERE, "build", "libhbmprobe.so"))
     vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
-    Pr.acm_probe_mimic.argtypes = [sz, vp, vp, vp, vp, ci, ci, vp]
+    Pr.acm_probe_mimic.argtypes = [sz, vp, vp, vp, vp, ci, ci, ci, vp]
     sh = torch.cuda.current_stream().cuda_stream
     params, (w, h) = samples.SAMPLES[2]
     cam = _lib.AcmCamera()
@@ -52,7 +52,7 @@ def main():
             for nt in (0, 1):
                 def mim():
                     Pr.acm_probe_mimic(n, pts.data_ptr(), uv.data_ptr(), st.data_ptr(),
-                                       jac.data_ptr(), 8, nt, sh)
+                                       jac.data_ptr(), 8, nt, 0, sh)
                 L.acm_set_tuning(_lib.TUNE_PROJECT_VARIANT, nt)
 
                 def real(al):

@@ -30,7 +30,7 @@ def main():
     vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     L.acm_probe_read.argtypes = [vp, sz, vp, ci, ci, ci, vp]
     L.acm_probe_write.argtypes = [vp, sz, ci, vp]
-    L.acm_probe_mimic.argtypes = [sz, vp, vp, vp, vp, ci, ci, vp]
+    L.acm_probe_mimic.argtypes = [sz, vp, vp, vp, vp, ci, ci, ci, vp]
     sh = torch.cuda.current_stream().cuda_stream
     n = a.points
     cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -73,7 +73,7 @@ def main():
         cell(f"write_{wb >> 20}MiB_{'nt' if nt else 'plain'}",
              lambda: L.acm_probe_write(buf.data_ptr(), wb, nt, sh), wb)
     del buf
-    xyz = torch.rand((n, 3), dtype=torch.float64, device="cuda")
+    xyz = torch.rand((5 * n,), dtype=torch.float64, device="cuda")  # points, then obs
     uv = torch.empty((n, 2), dtype=torch.float64, device="cuda")
     st = torch.empty((n,), dtype=torch.uint8, device="cuda")
     jac = torch.empty((9, n, 2), dtype=torch.float64, device="cuda")
@@ -81,8 +81,13 @@ def main():
         for nt in (0, 1):
             cell(f"mimic_project_J{cols}_{'nt' if nt else 'plain'}",
                  lambda: L.acm_probe_mimic(n, xyz.data_ptr(), uv.data_ptr(), st.data_ptr(),
-                                           jac.data_ptr(), cols, nt, sh),
+                                           jac.data_ptr(), cols, nt, 0, sh),
                  (24 + 16 + 1 + 16 * cols) * n)
+    for cols in (6, 8):  # residual + J traffic: + 16 B observation read per point
+        cell(f"mimic_residual_J{cols}_nt",
+             lambda: L.acm_probe_mimic(n, xyz.data_ptr(), uv.data_ptr(), st.data_ptr(),
+                                       jac.data_ptr(), cols, 1, 1, sh),
+             (24 + 16 + 16 + 1 + 16 * cols) * n)
     print(json.dumps({"what": "HBM ceilings (zero-compute probes)", "points": n,
                       "device": torch.cuda.get_device_name(0), "cus": cus, "cells": out}))
 

@@ -52,13 +52,19 @@ __global__ __launch_bounds__(256) void k_write(double* __restrict__ p, size_t n2
     if (i < n2) put2<NT>(p + 2 * i, v, v);
 }
 
-template <bool NT, int COLS>
+// OBS: also read a 16-B observation per point (the residual kernel's traffic)
+template <bool NT, int COLS, bool OBS>
 __global__ __launch_bounds__(256) void k_mimic(size_t n, const double* __restrict__ xyz,
                                                double* __restrict__ uv, uint8_t* __restrict__ st,
                                                double* __restrict__ jac) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const double x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    double x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    if (OBS) {
+        const dbl2 o = *reinterpret_cast<const dbl2*>(xyz + 3 * n + 2 * i);
+        x += o.x;
+        y += o.y;
+    }
     put2<NT>(uv + 2 * i, x + z, y + z);
     if (NT) __builtin_nontemporal_store((uint8_t)(z < 0.0), st + i);
     else st[i] = (uint8_t)(z < 0.0);
@@ -96,14 +102,17 @@ int acm_probe_write(void* buf, size_t bytes, int nt, void* stream) {
     return (int)hipGetLastError();
 }
 
+// obs != 0: xyz must hold 3n + 2n doubles (points, then observations)
 int acm_probe_mimic(size_t n, const double* xyz, double* uv, uint8_t* st, double* jac, int cols,
-                    int nt, void* stream) {
+                    int nt, int obs, void* stream) {
     hipStream_t s = (hipStream_t)stream;
 #define MIMIC(C)                                                                          \
     if (cols == C) {                                                                      \
-        if (nt) hipLaunchKernelGGL((k_mimic<true, C>), dim3(blocks(n)), dim3(256), 0, s, n, \
-                                   xyz, uv, st, jac);                                     \
-        else hipLaunchKernelGGL((k_mimic<false, C>), dim3(blocks(n)), dim3(256), 0, s, n,  \
+        if (obs) hipLaunchKernelGGL((k_mimic<true, C, true>), dim3(blocks(n)), dim3(256), 0, s, \
+                                    n, xyz, uv, st, jac);                                 \
+        else if (nt) hipLaunchKernelGGL((k_mimic<true, C, false>), dim3(blocks(n)), dim3(256), 0, \
+                                        s, n, xyz, uv, st, jac);                          \
+        else hipLaunchKernelGGL((k_mimic<false, C, false>), dim3(blocks(n)), dim3(256), 0, s, n, \
                                 xyz, uv, st, jac);                                        \
         return (int)hipGetLastError();                                                    \
     }
