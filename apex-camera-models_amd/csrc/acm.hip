@@ -132,15 +132,17 @@ __device__ __forceinline__ void st1(uint8_t* p, uint8_t v) {
     else *p = v;
 }
 
-// Tuning variants of the project kernel (bit flags, see acm_set_tuning):
+// Tuning variants of the direct project kernel (bit flags, see acm_set_tuning):
 //   kVarNT     non-temporal stores for the write-once outputs
 //   kVarGrid   persistent grid-stride launch (8 workgroups per CU)
-//   kVarTwo    two points per lane (both loads issued before either compute)
-// Default (-1, "auto"): non-temporal stores once the outputs exceed the
-// 256 MiB Infinity Cache (they cannot stay cache-resident for a consumer
-// anyway); measured 0.252 vs 0.312 ms for 10M-point KB project+J
-// (profiles/r01_sweep_project.log).
-enum { kVarNT = 1, kVarGrid = 2, kVarTwo = 4 };
+//   kVarNTL    non-temporal loads of the point stream
+// Default (-1, "auto"): non-temporal stores once the outputs exceed
+// kNtThresholdBytes (0.252 vs 0.312 ms for 10M-point KB project+J,
+// profiles/r01_sweep_project.log), plain loads (nt loads measured 20%
+// slower beside the store stream, profiles/r01_diag_ntl.log).  (+J launches
+// go to k_project_al unless ACM_TUNE_ALIGN_J = 0.)  A two-points-per-lane
+// variant measured no gain and was dropped.
+enum { kVarNT = 1, kVarGrid = 2, kVarNTL = 4 };
 static int g_project_variant = -1;
 // Residual+J: plain stores by default.  Unlike project+J, non-temporal stores
 // measured slower here (DS, 9.3M points: 0.273 ms plain vs 0.310 ms nt,
@@ -158,9 +160,17 @@ static int g_align_j = -1;
 // k_normal_eq: -1 = auto (on), 0 = off, 1 = on (5-11% faster, read probe
 // 6.9 vs 6.3 TB/s; profiles/r01_ne_sweep.log, r01_hbm_ceiling.log).
 static int g_nt_loads = -1;
+// Non-temporal loads of the pixel stream in k_unproject (-1 auto = off, 0,
+// 1): beside the non-temporal ray stores they measured 2-25% slower for
+// every model (profiles/r01_diag_ntl.log).
+static int g_nt_loads_unproject = -1;
 // FOV grid search: points per lane step (1, 2, 4).
 static int g_fov_unroll = 2;
-constexpr size_t kNtThresholdBytes = 256ull << 20;
+// Outputs above this many bytes are stored non-temporally.  Measured at 10M
+// points (profiles/r01_diag_ntl.log): project without J (170 MB out) 0.056 ms
+// nt vs 0.072 plain; a consumer that re-reads a smaller output soon after
+// still finds it in the 256 MiB Infinity Cache with plain stores.
+constexpr size_t kNtThresholdBytes = 64ull << 20;
 
 template <class TagT, int LAYOUT, bool WJ, bool NT>
 __device__ __forceinline__ void project_point(const Cam<double>& c, size_t n, size_t i, double x,
@@ -188,26 +198,20 @@ __global__ __launch_bounds__(kBlock) void k_project(acm_camera cam, size_t n,
                                                     uint8_t* __restrict__ status,
                                                     double* __restrict__ jac) {
     constexpr bool NT = (VAR & kVarNT) != 0;
+    constexpr bool NTL = (VAR & kVarNTL) != 0;
     const Cam<double> c = make_cam<double>(cam);
-    if (VAR & kVarTwo) {
-        const size_t i0 = (size_t)blockIdx.x * (2 * kBlock) + threadIdx.x, i1 = i0 + kBlock;
-        double x0 = 0, y0 = 0, z0 = 1, x1 = 0, y1 = 0, z1 = 1;
-        if (i0 < n) load_point<LAYOUT>(pts, n, i0, x0, y0, z0);
-        if (i1 < n) load_point<LAYOUT>(pts, n, i1, x1, y1, z1);
-        if (i0 < n) project_point<TagT, LAYOUT, WJ, NT>(c, n, i0, x0, y0, z0, uv, status, jac);
-        if (i1 < n) project_point<TagT, LAYOUT, WJ, NT>(c, n, i1, x1, y1, z1, uv, status, jac);
-    } else if (VAR & kVarGrid) {
+    if (VAR & kVarGrid) {
         const size_t stride = (size_t)gridDim.x * kBlock;
         for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
             double x, y, z;
-            load_point<LAYOUT>(pts, n, i, x, y, z);
+            load_point<LAYOUT, NTL>(pts, n, i, x, y, z);
             project_point<TagT, LAYOUT, WJ, NT>(c, n, i, x, y, z, uv, status, jac);
         }
     } else {
         const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
         if (i >= n) return;
         double x, y, z;
-        load_point<LAYOUT>(pts, n, i, x, y, z);
+        load_point<LAYOUT, NTL>(pts, n, i, x, y, z);
         project_point<TagT, LAYOUT, WJ, NT>(c, n, i, x, y, z, uv, status, jac);
     }
 }
@@ -392,7 +396,7 @@ __device__ __forceinline__ void st1d(double* p, double v) {
     else *p = v;
 }
 
-template <class TagT, int LAYOUT, bool NT>
+template <class TagT, int LAYOUT, bool NT, bool NTL>
 __global__ __launch_bounds__(kBlock) void k_unproject(acm_camera cam, size_t n,
                                                       const double* __restrict__ uv,
                                                       double* __restrict__ rays,
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void k_unproject(acm_camera cam, size_t n,
     const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const Cam<double> c = make_cam<double>(cam);
-    const double2 q = *reinterpret_cast<const double2*>(uv + 2 * i);
+    const double2 q = ld2<NTL>(uv + 2 * i);
     double X, Y, Z;
     const uint8_t st = M::unproject(c, q.x, q.y, X, Y, Z);
     if (st != ST_OK) X = Y = Z = __builtin_nan("");
@@ -1482,7 +1486,7 @@ ACM_API int acm_project(const acm_camera* cam, size_t n, const double* points_3d
     if (var < 0) {
         const size_t out_bytes =
             n * (17 + (jacobian ? 16 * (size_t)acm_num_params(cam->model) : 0));
-        var = out_bytes > kNtThresholdBytes ? kVarNT : 0;
+        var = (out_bytes > kNtThresholdBytes ? kVarNT : 0) | (g_nt_loads == 1 ? kVarNTL : 0);
     }
     const int P = acm_num_params(cam->model);
     (void)P;
@@ -1505,8 +1509,7 @@ ACM_API int acm_project(const acm_camera* cam, size_t n, const double* points_3d
             constexpr int L = decltype(lay_c)::value;
             constexpr bool WJ = decltype(wj_c)::value;
             constexpr int V = decltype(var_c)::value;
-            unsigned blocks = (V & kVarTwo) ? (unsigned)((n + 2 * kBlock - 1) / (2 * kBlock))
-                                            : grid_for(n);
+            unsigned blocks = grid_for(n);
             if ((V & kVarGrid) && blocks > 256u * 8u) blocks = 256u * 8u;
             hipLaunchKernelGGL((k_project<TagT, L, WJ, V>), dim3(blocks), dim3(kBlock), 0, s,
                                prep(*cam), n, points_3d, points_2d, status, jacobian);
@@ -1518,6 +1521,8 @@ ACM_API int acm_project(const acm_camera* cam, size_t n, const double* points_3d
             case 3: launch(lay_c, wj_c, std::integral_constant<int, 3>{}); break;
             case 4: launch(lay_c, wj_c, std::integral_constant<int, 4>{}); break;
             case 5: launch(lay_c, wj_c, std::integral_constant<int, 5>{}); break;
+            case 6: launch(lay_c, wj_c, std::integral_constant<int, 6>{}); break;
+            case 7: launch(lay_c, wj_c, std::integral_constant<int, 7>{}); break;
             default: launch(lay_c, wj_c, std::integral_constant<int, 0>{}); break;
             }
         };
@@ -1574,11 +1579,15 @@ ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_
         using TagT = decltype(tag);
         const dim3 g(grid_for(n)), b(kBlock);
         const bool nt = n * 25 > kNtThresholdBytes;  // rays + status written once
-#define ACM_UNP(L, NT) \
-    hipLaunchKernelGGL((k_unproject<TagT, L, NT>), g, b, 0, s, prep(*cam), n, points_2d, rays, status)
-        if (layout == ACM_LAYOUT_AOS) { if (nt) ACM_UNP(ACM_LAYOUT_AOS, true); else ACM_UNP(ACM_LAYOUT_AOS, false); }
-        else { if (nt) ACM_UNP(ACM_LAYOUT_SOA, true); else ACM_UNP(ACM_LAYOUT_SOA, false); }
-#undef ACM_UNP
+        const bool ntl = g_nt_loads_unproject == 1;
+        auto go = [&](auto lay_c) {
+            constexpr int L = decltype(lay_c)::value;
+            auto kern = nt ? (ntl ? k_unproject<TagT, L, true, true> : k_unproject<TagT, L, true, false>)
+                           : (ntl ? k_unproject<TagT, L, false, true> : k_unproject<TagT, L, false, false>);
+            hipLaunchKernelGGL(kern, g, b, 0, s, prep(*cam), n, points_2d, rays, status);
+        };
+        if (layout == ACM_LAYOUT_AOS) go(std::integral_constant<int, ACM_LAYOUT_AOS>{});
+        else go(std::integral_constant<int, ACM_LAYOUT_SOA>{});
         return check_launch("acm_unproject");
     });
 }
@@ -2036,8 +2045,8 @@ ACM_API int acm_stream_synchronize(void* stream) {
 
 ACM_API int acm_set_tuning(int key, int value) {
     if (key == ACM_TUNE_PROJECT_VARIANT) {
-        if (value < -1 || value > 5)
-            return fail(ACM_ERR_INVALID_ARGUMENT, "variant must be -1 (auto) or 0..5");
+        if (value < -1 || value > 7)
+            return fail(ACM_ERR_INVALID_ARGUMENT, "variant must be -1 (auto) or 0..7");
         const int old = g_project_variant;
         g_project_variant = value;
         return old;
@@ -2072,6 +2081,12 @@ ACM_API int acm_set_tuning(int key, int value) {
         if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
         const int old = g_nt_loads;
         g_nt_loads = value;
+        return old;
+    }
+    if (key == ACM_TUNE_NT_LOADS_UNPROJECT) {
+        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
+        const int old = g_nt_loads_unproject;
+        g_nt_loads_unproject = value;
         return old;
     }
     if (key == ACM_TUNE_FOV_UNROLL) {

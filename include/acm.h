@@ -354,9 +354,9 @@ ACM_API int acm_stream_synchronize(void *stream);
 
 /* Process-wide kernel tuning knob (benchmark sweeps; results are identical
  * for every setting).  ACM_TUNE_PROJECT_VARIANT: bit flags of acm_project's
- * kernel, 1 = non-temporal stores, 2 = persistent grid-stride launch,
- * 4 = two points per lane; -1 (default) = auto (non-temporal stores when the
- * outputs exceed 256 MiB).  ACM_TUNE_RESIDUAL_NT: non-temporal stores in
+ * direct kernel, 1 = non-temporal stores, 2 = persistent grid-stride launch,
+ * 4 = non-temporal loads; -1 (default) = auto (non-temporal stores when the
+ * outputs exceed 64 MiB; non-temporal loads only if ACM_TUNE_NT_LOADS = 1).  ACM_TUNE_RESIDUAL_NT: non-temporal stores in
  * acm_residual_jacobian (-1 auto, 0 off = default, 1 on).  ACM_TUNE_NE_WAVES:
  * minimum waves per SIMD the normal-equations kernel is compiled for
  * (0 = per-model default, 1, 3, 4).  ACM_TUNE_FOV_UNROLL: points per lane step of the FOV
@@ -366,7 +366,9 @@ ACM_API int acm_stream_synchronize(void *stream);
  * acm_residual_jacobian: -1 = auto (default) = line-aligned store windows
  * through LDS, 0 = one point per lane with direct stores, 1 = aligned.
  * ACM_TUNE_NT_LOADS: non-temporal loads of the point / observation streams
- * in the normal-equations kernel (-1 = auto = on, 0, 1).
+ * in the normal-equations kernel (-1 = auto = on, 0, 1; 1 also turns them
+ * on in the direct project kernel).  ACM_TUNE_NT_LOADS_UNPROJECT: the same
+ * for acm_unproject's pixel stream (-1 = auto = off, 0, 1).
  * Returns the previous value or an error. */
 enum {
     ACM_TUNE_PROJECT_VARIANT = 0,
@@ -375,7 +377,8 @@ enum {
     ACM_TUNE_FOV_UNROLL = 3,
     ACM_TUNE_NE_UNROLL = 4,
     ACM_TUNE_ALIGN_J = 5,
-    ACM_TUNE_NT_LOADS = 6
+    ACM_TUNE_NT_LOADS = 6,
+    ACM_TUNE_NT_LOADS_UNPROJECT = 7
 };
 ACM_API int acm_set_tuning(int key, int value);
 
