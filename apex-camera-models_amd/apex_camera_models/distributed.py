@@ -106,7 +106,7 @@ def combine_reprojection_stats(local_errors: torch.Tensor, group=None) -> dict:
 def distributed_median(local_errors: torch.Tensor, n_valid_global: int, group=None) -> float:
     """Exact median of the union of every rank's non-NaN errors
     (error_metrics.rs:103-111): acm_median_valid_allreduce, one all-reduce of
-    a 256-bin histogram per radix pass (16 x 2 KB, latency-bound)."""
+    the 2 x 2048-bin histogram per radix pass (6 x 32 KB, latency-bound)."""
     import ctypes
 
     from . import _lib

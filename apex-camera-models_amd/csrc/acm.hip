@@ -871,19 +871,30 @@ __device__ __forceinline__ bool sample_cell(const Cam<double>& c, const Grid& g,
     return st == ST_OK && Z > 0.0;  // :91-94
 }
 
+// Each workgroup owns kSampleCells consecutive cells (kSampleR rounds of 256):
+// few enough workgroups that the scan of their counts is a handful of
+// coalesced tiles, and round r of lane t is cell base + 256 r + t, so the
+// write pass emits kept points in cell order.
+constexpr int kSampleR = 16;
+constexpr size_t kSampleCells = (size_t)kBlock * kSampleR;
+
 template <class TagT>
 __global__ __launch_bounds__(kBlock) void k_sample_count(acm_camera cam, Grid g, size_t cells,
                                                          uint64_t* __restrict__ counts) {
     const Cam<double> c = make_cam<double>(cam);
-    const size_t cell = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    bool keep = false;
-    if (cell < cells) {
-        double u, v, X, Y, Z;
-        keep = sample_cell<TagT>(c, g, cell, u, v, X, Y, Z);
+    const size_t base = (size_t)blockIdx.x * kSampleCells;
+    uint32_t mine = 0;
+    for (int r = 0; r < kSampleR; ++r) {
+        const size_t cell = base + (size_t)r * kBlock + threadIdx.x;
+        if (cell < cells) {
+            double u, v, X, Y, Z;
+            mine += sample_cell<TagT>(c, g, cell, u, v, X, Y, Z) ? 1u : 0u;
+        }
     }
-    const uint64_t m = __ballot(keep);
     __shared__ uint32_t sm[kBlock / 64];
-    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off, 64);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = mine;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t t = 0;
@@ -892,32 +903,37 @@ __global__ __launch_bounds__(kBlock) void k_sample_count(acm_camera cam, Grid g,
     }
 }
 
-// exclusive scan of nb block counts by one workgroup of 1024 lanes
+// Exclusive scan of nb workgroup counts by one workgroup of 1024 lanes, in
+// coalesced tiles of 1024 (wave shuffle scan + a 16-entry LDS scan per tile).
 __global__ __launch_bounds__(1024) void k_scan_counts(const uint64_t* __restrict__ counts,
                                                       size_t nb, uint64_t* __restrict__ offsets,
                                                       uint64_t* __restrict__ out_counts,
                                                       uint64_t cells) {
-    const size_t per = (nb + 1023) / 1024;
-    const size_t b0 = (size_t)threadIdx.x * per;
-    uint64_t s = 0;
-    for (size_t b = b0; b < b0 + per && b < nb; ++b) s += counts[b];
-    __shared__ uint64_t sm[1024];
-    sm[threadIdx.x] = s;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over the 1024 thread sums
-    for (int off = 1; off < 1024; off <<= 1) {
-        uint64_t t = threadIdx.x >= (unsigned)off ? sm[threadIdx.x - off] : 0;
+    __shared__ uint64_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    uint64_t carry = 0;
+    for (size_t tile = 0; tile < nb; tile += 1024) {
+        const size_t b = tile + t;
+        const uint64_t c = b < nb ? counts[b] : 0;
+        uint64_t x = c;  // inclusive wave scan
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint64_t y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) wsum[wid] = x;
         __syncthreads();
-        sm[threadIdx.x] += t;
+        uint64_t before = 0, total = 0;
+        for (int w = 0; w < 16; ++w) {
+            if (w < wid) before += wsum[w];
+            total += wsum[w];
+        }
+        if (b < nb) offsets[b] = carry + before + x - c;
+        carry += total;
         __syncthreads();
     }
-    uint64_t run = sm[threadIdx.x] - s;  // exclusive prefix of this thread's run
-    for (size_t b = b0; b < b0 + per && b < nb; ++b) {
-        offsets[b] = run;
-        run += counts[b];
-    }
-    if (threadIdx.x == 1023) {
-        out_counts[0] = sm[1023];
+    if (t == 0) {
+        out_counts[0] = carry;
         out_counts[1] = cells;
     }
 }
@@ -928,24 +944,33 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(acm_camera cam, Grid g,
                                                          double* __restrict__ uv_out,
                                                          double* __restrict__ xyz_out) {
     const Cam<double> c = make_cam<double>(cam);
-    const size_t cell = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    bool keep = false;
-    double u = 0, v = 0, X = 0, Y = 0, Z = 0;
-    if (cell < cells) keep = sample_cell<TagT>(c, g, cell, u, v, X, Y, Z);
-    const uint64_t m = __ballot(keep);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     __shared__ uint32_t sm[kBlock / 64];
-    if (lane == 0) sm[wid] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint64_t base = offsets[blockIdx.x];
-    for (int w = 0; w < wid; ++w) base += sm[w];
-    const uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
-    if (keep) {
-        const size_t k = base + (uint64_t)__popcll(below);
-        *reinterpret_cast<double2*>(uv_out + 2 * k) = make_double2(u, v);
-        xyz_out[3 * k] = X;
-        xyz_out[3 * k + 1] = Y;
-        xyz_out[3 * k + 2] = Z;
+    const size_t base = (size_t)blockIdx.x * kSampleCells;
+    uint64_t run = offsets[blockIdx.x];
+    for (int r = 0; r < kSampleR; ++r) {
+        const size_t cell = base + (size_t)r * kBlock + threadIdx.x;
+        bool keep = false;
+        double u = 0, v = 0, X = 0, Y = 0, Z = 0;
+        if (cell < cells) keep = sample_cell<TagT>(c, g, cell, u, v, X, Y, Z);
+        const uint64_t m = __ballot(keep);
+        if (lane == 0) sm[wid] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint64_t wbase = run, tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            if (w < wid) wbase += sm[w];
+            tot += sm[w];
+        }
+        const uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+        if (keep) {
+            const size_t k = wbase + (uint64_t)__popcll(below);
+            *reinterpret_cast<double2*>(uv_out + 2 * k) = make_double2(u, v);
+            xyz_out[3 * k] = X;
+            xyz_out[3 * k + 1] = Y;
+            xyz_out[3 * k + 2] = Z;
+        }
+        run += tot;
+        __syncthreads();  // sm is rewritten next round
     }
 }
 
@@ -959,52 +984,190 @@ struct SelState {
     unsigned long long prefix, mask, k;
 };
 
-// Histogram counts are kept as f64 (exact below 2^53, and integer sums are
-// order-independent) so a multi-GPU caller can all-reduce them in place with
-// the same f64 callback the LM uses.
-__global__ __launch_bounds__(kBlock) void k_sel_hist(size_t n, const double* __restrict__ vals,
-                                                     const SelState* __restrict__ st, int shift,
-                                                     double* __restrict__ hist) {
-    __shared__ unsigned int h[256];
-    h[threadIdx.x] = 0;  // kBlock == 256
-    __syncthreads();
-    const unsigned long long prefix = st->prefix, mask = st->mask;
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        const unsigned long long b = (unsigned long long)__double_as_longlong(vals[i]);
-        if ((b & mask) == prefix) atomicAdd(&h[(b >> shift) & 0xFFull], 1u);
+// Exact radix select on the f64 bit patterns (values are >= 0 or NaN, so the
+// unsigned order of the bits is the numeric order and NaNs sort last).  Both
+// median ranks, (m-1)/2 (state a) and m/2 (state b), are selected in the
+// same passes: each pass reads the values once and builds one 2048-bin
+// histogram per state (11-bit digits: 6 passes over the values instead of
+// 2 x 8 with 8-bit digits).  Histogram counts are kept as f64 (exact below
+// 2^53, and integer sums are order-independent) so a multi-GPU caller can
+// all-reduce them in place with the same f64 callback the LM uses.
+constexpr int kSelBits = 11, kSelBins = 1 << kSelBits;
+// digit p covers bits [shift, shift + width): 53..63, 42..52, 31..41, 20..30, 9..19, 0..8
+__host__ __device__ constexpr int sel_shift(int pass) { return pass < 5 ? 53 - 11 * pass : 0; }
+__host__ __device__ constexpr int sel_width(int pass) { return pass < 5 ? 11 : 9; }
+constexpr int kSelPasses = 6;
+constexpr int kSelU = 8;  // values in flight per lane in the streaming passes
+
+// One LDS histogram increment per lane with pred, aggregated across the wave
+// when AGG: lanes holding the same digit add their count with one atomic
+// (pass 0's digits are the exponent: a wave's 64 values share a handful of
+// them, and 64 same-address LDS atomics would serialise).
+template <bool AGG>
+__device__ __forceinline__ void sel_count(unsigned int* h, bool pred, unsigned d) {
+    if (!AGG) {
+        if (pred) atomicAdd(&h[d], 1u);
+        return;
     }
-    __syncthreads();
-    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (double)h[threadIdx.x]);
+    unsigned long long act = __ballot(pred);
+    const int lane = threadIdx.x & 63;
+    while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const unsigned dl = (unsigned)__shfl((int)d, leader, 64);
+        const unsigned long long same = __ballot(pred && d == dl) & act;
+        if (lane == leader) atomicAdd(&h[dl], (unsigned)__popcll(same));
+        act &= ~same;
+    }
 }
 
-__global__ void k_sel_pick(SelState* __restrict__ st, int shift, double* __restrict__ hist) {
-    if (threadIdx.x != 0) return;
-    unsigned long long k = st->k, run = 0;
-    int b = 0;
-    for (; b < 256; ++b) {
-        const unsigned long long c = (unsigned long long)hist[b];
-        if (run + c > k) break;
-        run += c;
+// n_dev != nullptr: the value count lives in device memory (the compacted
+// candidate buffer of the later passes).
+template <bool AGG>
+__global__ __launch_bounds__(kBlock) void k_sel_hist(size_t n, const unsigned long long* n_dev,
+                                                     const double* __restrict__ vals,
+                                                     const SelState* __restrict__ st, int pass,
+                                                     double* __restrict__ hist) {
+    __shared__ unsigned int h[2][kSelBins];
+    for (int j = threadIdx.x; j < 2 * kSelBins; j += kBlock) (&h[0][0])[j] = 0;
+    __syncthreads();
+    if (n_dev) n = (size_t)*n_dev;
+    const unsigned long long pa = st[0].prefix, ma = st[0].mask;
+    const unsigned long long pb = st[1].prefix, mb = st[1].mask;
+    const bool same = pa == pb && ma == mb;  // one histogram serves both states
+    const int shift = sel_shift(pass);
+    const unsigned long long dmask = (1ull << sel_width(pass)) - 1;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    // whole waves iterate together (the AGG ballots need every lane); kSelU
+    // loads in flight per lane
+    for (size_t i0 = (size_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); i0 < n;
+         i0 += kSelU * stride) {
+        unsigned long long bits[kSelU];
+#pragma unroll
+        for (int u = 0; u < kSelU; ++u) {
+            const size_t i = i0 + u * stride + (threadIdx.x & 63);
+            bits[u] = i < n ? (unsigned long long)__double_as_longlong(vals[i]) : ~0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kSelU; ++u) {
+            const bool in = i0 + u * stride + (threadIdx.x & 63) < n;
+            const unsigned d = (unsigned)((bits[u] >> shift) & dmask);
+            sel_count<AGG>(h[0], in && (bits[u] & ma) == pa, d);
+            if (!same) sel_count<AGG>(h[1], in && (bits[u] & mb) == pb, d);
+        }
     }
-    if (b == 256) b = 255;
-    st->k = k - run;
-    st->prefix |= (unsigned long long)b << shift;
-    st->mask |= 0xFFull << shift;
-    for (int j = 0; j < 256; ++j) hist[j] = 0.0;
+    __syncthreads();
+    for (int j = threadIdx.x; j < kSelBins; j += kBlock) {
+        const unsigned c0 = h[0][j];
+        const unsigned c1 = same ? c0 : h[1][j];
+        if (c0) atomicAdd(&hist[j], (double)c0);
+        if (c1) atomicAdd(&hist[kSelBins + j], (double)c1);
+    }
+}
+
+// Candidates of either state (values matching its prefix after the first
+// passes) appended to a compact buffer; later passes read only those.  The
+// buffer order depends on scheduling, the selected ranks do not.
+__global__ __launch_bounds__(kBlock) void k_sel_compact(size_t n, const double* __restrict__ vals,
+                                                        const SelState* __restrict__ st,
+                                                        double* __restrict__ cbuf,
+                                                        unsigned long long* __restrict__ count) {
+    const unsigned long long pa = st[0].prefix, ma = st[0].mask;
+    const unsigned long long pb = st[1].prefix, mb = st[1].mask;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    const int lane = threadIdx.x & 63;
+    for (size_t i0 = (size_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); i0 < n;
+         i0 += kSelU * stride) {
+        double v[kSelU];
+#pragma unroll
+        for (int u = 0; u < kSelU; ++u) {
+            const size_t i = i0 + u * stride + lane;
+            v[u] = i < n ? vals[i] : 0.0;
+        }
+        // one global atomic per wave per kSelU values (a single counter
+        // address: fewer atomics, less serialisation)
+        unsigned long long m[kSelU];
+        unsigned total = 0;
+#pragma unroll
+        for (int u = 0; u < kSelU; ++u) {
+            const bool in = i0 + u * stride + lane < n;
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(v[u]);
+            m[u] = __ballot(in && ((bits & ma) == pa || (bits & mb) == pb));
+            total += (unsigned)__popcll(m[u]);
+        }
+        if (!total) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(count, (unsigned long long)total);
+        base = __shfl((long long)base, 0, 64);
+        const unsigned long long below = (1ull << lane) - 1;
+#pragma unroll
+        for (int u = 0; u < kSelU; ++u) {
+            if ((m[u] >> lane) & 1ull) cbuf[base + __popcll(m[u] & below)] = v[u];
+            base += (unsigned long long)__popcll(m[u]);
+        }
+    }
+}
+
+// Picks this pass's digit for both states from the (all-reduced) histograms
+// and clears them for the next pass.  One workgroup: each lane owns 8
+// consecutive bins, a block-wide inclusive scan finds the bin where the
+// running count passes k.
+__global__ __launch_bounds__(kBlock) void k_sel_pick(SelState* __restrict__ st, int pass,
+                                                     double* __restrict__ hist) {
+    constexpr int PER = kSelBins / kBlock;
+    __shared__ unsigned long long scan[kBlock];
+    __shared__ int found;
+    const int t = threadIdx.x;
+    const int shift = sel_shift(pass);
+    const unsigned long long dmask = (1ull << sel_width(pass)) - 1;
+    for (int w = 0; w < 2; ++w) {
+        double* hw = hist + w * kSelBins;
+        unsigned long long mine = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) mine += (unsigned long long)hw[t * PER + j];
+        scan[t] = mine;
+        if (t == 0) found = kBlock - 1;
+        __syncthreads();
+        for (int off = 1; off < kBlock; off <<= 1) {  // Hillis-Steele inclusive scan
+            const unsigned long long v = t >= off ? scan[t - off] : 0;
+            __syncthreads();
+            scan[t] += v;
+            __syncthreads();
+        }
+        const unsigned long long k = st[w].k;
+        const unsigned long long before = t ? scan[t - 1] : 0;
+        if (before <= k && k < scan[t]) found = t;  // exactly one lane, unless k >= total
+        __syncthreads();
+        if (t == found) {
+            unsigned long long run = t ? scan[t - 1] : 0;
+            int b = t * PER + PER - 1;
+            for (int j = 0; j < PER; ++j) {
+                const unsigned long long c = (unsigned long long)hw[t * PER + j];
+                if (run + c > k) { b = t * PER + j; break; }
+                run += c;
+            }
+            st[w].k = k - run;
+            st[w].prefix |= (unsigned long long)b << shift;
+            st[w].mask |= dmask << shift;
+        }
+        __syncthreads();
+    }
+    for (int j = t; j < 2 * kSelBins; j += kBlock) hist[j] = 0.0;
 }
 
 __global__ void k_sel_init(SelState* __restrict__ st, const double* __restrict__ nvalid_src,
-                           unsigned long long nvalid_fixed, int which,
-                           double* __restrict__ hist) {
-    if (threadIdx.x != 0) return;
+                           unsigned long long nvalid_fixed, double* __restrict__ hist,
+                           unsigned long long* __restrict__ count) {
     const unsigned long long m =
         nvalid_src ? (unsigned long long)nvalid_src[0] : nvalid_fixed;
-    // which 0: rank (m-1)/2 ; which 1: rank m/2  (equal for odd m)
-    st->k = which == 0 ? (m ? (m - 1) / 2 : 0) : m / 2;
-    st->prefix = 0;
-    st->mask = 0;
-    for (int j = 0; j < 256; ++j) hist[j] = 0.0;
+    if (threadIdx.x == 0) {
+        *count = 0;
+        // state a: rank (m-1)/2 ; state b: rank m/2  (equal for odd m)
+        st[0].k = m ? (m - 1) / 2 : 0;
+        st[1].k = m / 2;
+        st[0].prefix = st[1].prefix = 0;
+        st[0].mask = st[1].mask = 0;
+    }
+    for (int j = threadIdx.x; j < 2 * kSelBins; j += blockDim.x) hist[j] = 0.0;
 }
 
 __global__ void k_sel_finish(const SelState* __restrict__ a, const SelState* __restrict__ b,
@@ -1764,8 +1927,8 @@ ACM_API size_t acm_sample_points_workspace_size(const acm_camera* cam, size_t n_
     uint32_t ncx, ncy;
     if (!cam || acm_sample_points_grid(cam->width, cam->height, n_requested, &ncx, &ncy))
         return 0;
-    const size_t nb = ((size_t)ncx * ncy + kBlock - 1) / kBlock;
-    return 2 * nb * sizeof(uint64_t);
+    const size_t nb = ((size_t)ncx * ncy + kSampleCells - 1) / kSampleCells;
+    return 2 * (nb ? nb : 1) * sizeof(uint64_t);
 }
 
 ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, size_t cell_begin,
@@ -1782,7 +1945,7 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
     if (!points_2d_out || !points_3d_out || !counts || !workspace)
         return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
     const size_t cells = cell_end - cell_begin;
-    const size_t nb = cells ? (cells + kBlock - 1) / kBlock : 1;
+    const size_t nb = cells ? (cells + kSampleCells - 1) / kSampleCells : 1;
     if (workspace_bytes < 2 * nb * sizeof(uint64_t))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "sample_points workspace too small");
     if (nb > 0x7fffffffull) return fail(ACM_ERR_INVALID_ARGUMENT, "sample grid too large");
@@ -1941,9 +2104,9 @@ ACM_API int acm_fov_grid_errors(const acm_camera* cam, size_t n, const double* p
     return check_launch("acm_fov_grid_errors");
 }
 
+// workspace: 2 SelState | 2 x 2048 f64 histogram | candidate count | n f64 candidates
 ACM_API size_t acm_median_workspace_size(size_t n) {
-    (void)n;
-    return 2 * sizeof(SelState) + 256 * sizeof(double);
+    return 2 * sizeof(SelState) + 2 * kSelBins * sizeof(double) + 16 + n * sizeof(double);
 }
 
 ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
@@ -1955,29 +2118,42 @@ ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
     if (workspace_bytes < acm_median_workspace_size(n))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "median workspace too small");
     hipStream_t s = (hipStream_t)stream;
-    SelState* sa = (SelState*)workspace;
-    SelState* sb = sa + 1;
-    double* hist = (double*)(sb + 1);
-    // <= 1024 workgroups: each flushes 256 histogram atomics per pass
+    SelState* st = (SelState*)workspace;
+    double* hist = (double*)(st + 2);
+    unsigned long long* count = (unsigned long long*)(hist + 2 * kSelBins);
+    double* cbuf = (double*)(count + 2);
+    // <= 1024 workgroups: each flushes its non-empty bins with f64 atomics
     const unsigned nb = (unsigned)std::min(
-        std::min(ne_blocks(n), 1024), resident_blocks(reinterpret_cast<const void*>(k_sel_hist)));
-    for (int which = 0; which < 2; ++which) {
-        SelState* st = which ? sb : sa;
-        hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, s, st, n_valid_device,
-                           (unsigned long long)n_valid, which, hist);
-        for (int shift = 56; shift >= 0; shift -= 8) {
-            hipLaunchKernelGGL(k_sel_hist, dim3(nb), dim3(kBlock), 0, s, n, values, st, shift,
-                               hist);
-            if (allreduce) {  // every rank then picks the same digit
-                int rc = check_launch("acm_median_valid (histogram)");
-                if (rc) return rc;
-                if (allreduce(allreduce_ctx, hist, 256, stream) != 0)
-                    return fail(ACM_ERR_INVALID_ARGUMENT, "allreduce callback failed");
-            }
-            hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(64), 0, s, st, shift, hist);
+        std::min(ne_blocks(n), 1024),
+        resident_blocks(reinterpret_cast<const void*>(k_sel_hist<true>)));
+    // passes 0-1 read every value (pass 0 aggregates its exponent digits per
+    // wave); then the candidates sharing either state's 22-bit prefix are
+    // compacted and passes 2-5 read only them.
+    constexpr int kFullPasses = 2;
+    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(kBlock), 0, s, st, n_valid_device,
+                       (unsigned long long)n_valid, hist, count);
+    for (int pass = 0; pass < kSelPasses; ++pass) {
+        if (pass == kFullPasses)
+            hipLaunchKernelGGL(k_sel_compact, dim3(nb), dim3(kBlock), 0, s, n, values, st, cbuf,
+                               count);
+        if (pass == 0)
+            hipLaunchKernelGGL(k_sel_hist<true>, dim3(nb), dim3(kBlock), 0, s, n, nullptr, values,
+                               st, pass, hist);
+        else if (pass < kFullPasses)
+            hipLaunchKernelGGL(k_sel_hist<false>, dim3(nb), dim3(kBlock), 0, s, n, nullptr,
+                               values, st, pass, hist);
+        else
+            hipLaunchKernelGGL(k_sel_hist<false>, dim3(std::min(nb, 256u)), dim3(kBlock), 0, s,
+                               (size_t)0, count, cbuf, st, pass, hist);
+        if (allreduce) {  // every rank then picks the same digits
+            int rc = check_launch("acm_median_valid (histogram)");
+            if (rc) return rc;
+            if (allreduce(allreduce_ctx, hist, 2 * kSelBins, stream) != 0)
+                return fail(ACM_ERR_INVALID_ARGUMENT, "allreduce callback failed");
         }
+        hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(kBlock), 0, s, st, pass, hist);
     }
-    hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(64), 0, s, sa, sb, n_valid_device,
+    hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(64), 0, s, st, st + 1, n_valid_device,
                        (unsigned long long)n_valid, out);
     return check_launch("acm_median_valid");
 }

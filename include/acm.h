@@ -290,10 +290,13 @@ ACM_API int acm_lm_optimize(acm_camera *cam, size_t n, const double *points_3d,
  * acm_reprojection_stats, else the host value n_valid).  Values must be
  * >= 0 or NaN.  out: device f64.
  * acm_median_valid_allreduce is the multi-GPU form: `values` is this
- * rank's shard, n_valid the GLOBAL count, and after each of the 16
- * histogram passes the 256-bin f64 histogram (device) goes through the
- * allreduce callback (a sum over ranks), so every rank selects the same
- * digits and returns the median of the union. */
+ * rank's shard, n_valid the GLOBAL count, and after each of the 6
+ * histogram passes the 2 x 2048-bin f64 histogram (device; both median
+ * ranks, 11-bit digits) goes through the allreduce callback (a sum over
+ * ranks), so every rank selects the same digits and returns the median of
+ * the union.  Two passes read all n values; the candidates sharing the
+ * selected 22-bit prefix are then compacted into the workspace (which is
+ * sized for n of them) and the last four passes read only those. */
 ACM_API size_t acm_median_workspace_size(size_t n);
 ACM_API int acm_median_valid(size_t n, const double *values,
                              const double *n_valid_device, uint64_t n_valid,

@@ -350,3 +350,47 @@ def test_buffers_at_8_byte_offsets(golden_dir, model):
     ref_r, ref_s2 = GpuBackend().unproject(model, params, w, h, g["uv_in"])
     assert np.array_equal(st2[1:].cpu().numpy(), ref_s2)
     assert np.array_equal(rays[1:].cpu().numpy().reshape(nu, 3), ref_r, equal_nan=True)
+
+
+def _gpu_median(vals):
+    import ctypes
+
+    import torch
+    from apex_camera_models import _lib
+    L = _lib.load()
+    v = torch.as_tensor(np.asarray(vals, dtype=np.float64), device="cuda")
+    n = v.numel()
+    m = int((~torch.isnan(v)).sum())
+    ws_b = L.acm_median_workspace_size(n)
+    ws = torch.empty(((ws_b + 7) // 8,), dtype=torch.float64, device="cuda")
+    out = torch.empty((1,), dtype=torch.float64, device="cuda")
+    _lib.check(L.acm_median_valid(n, v.data_ptr() if n else None, None, m, out.data_ptr(),
+                                  ws.data_ptr(), ws_b, None))
+    return float(out.item())
+
+
+@pytest.mark.parametrize("case", ["odd", "even", "ties", "tie_pair", "nan_mix", "one", "all_nan",
+                                  "denormal", "wide", "zeros", "big"])
+def test_median_radix_select_exact(case):
+    """acm_median_valid (6-pass 11-bit radix select, both ranks at once) is
+    the exact median of the non-NaN values, error_metrics.rs:103-111."""
+    rng = np.random.default_rng(hash(case) % 2**32)
+    v = {
+        "odd": rng.uniform(0, 5, 1001),
+        "even": rng.uniform(0, 5, 1000),
+        "ties": np.repeat(rng.uniform(0, 1, 37), 5),
+        "tie_pair": np.array([1.0, 2.0, 2.0, 3.0]),
+        "nan_mix": np.where(rng.uniform(size=5000) < 0.3, np.nan, rng.exponential(1.0, 5000)),
+        "one": np.array([0.125]),
+        "all_nan": np.full(17, np.nan),
+        "denormal": np.concatenate([np.full(10, 5e-324), np.full(11, 1e-310), [0.0] * 3]),
+        "wide": 10.0 ** rng.uniform(-300, 300, 4097),
+        "zeros": np.zeros(64),
+        "big": rng.exponential(0.01, 3_000_001),
+    }[case]
+    got = _gpu_median(v)
+    valid = v[~np.isnan(v)]
+    if valid.size == 0:
+        assert np.isnan(got)
+    else:
+        assert got == np.median(valid), (got, np.median(valid))

@@ -1,0 +1,54 @@
+"""Median radix-select timing / candidate count on config-5-like errors.
+
+  python tools/diag_median.py
+"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "apex-camera-models_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from apex_camera_models import KannalaBrandtModel, Resolution, _lib, conversion, samples, util
+    L = _lib.load()
+    kp, (w, h) = samples.SAMPLES[2]
+    src = KannalaBrandtModel._from_params(kp, Resolution(w, h))
+    uv, xyz = util.sample_points(src, 100_000_000)
+    n = xyz.shape[0]
+    model = conversion._init_target("double_sphere", src)
+    model.linear_estimation(xyz, uv)
+    errs = torch.empty((n,), dtype=torch.float64, device="cuda")
+    st = util.reprojection_stats(model, xyz, uv, errs)
+    ws_b = L.acm_median_workspace_size(n)
+    ws = torch.empty(((ws_b + 7) // 8,), dtype=torch.float64, device="cuda")
+    out = torch.empty((1,), dtype=torch.float64, device="cuda")
+    nv = int(st[5].item())
+
+    def med():
+        _lib.check(L.acm_median_valid(n, errs.data_ptr(), None, nv, out.data_ptr(),
+                                      ws.data_ptr(), ws_b, None))
+    for _ in range(3):
+        med()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        med()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    # candidate count lives right after the 2 states + 2 x 2048 histogram
+    cnt = ws.view(torch.int64)[(2 * 24) // 8 + 2 * 2048].item()
+    ref = float(torch.median(errs[~torch.isnan(errs)]).item())  # lower median
+    print(json.dumps({"what": "median", "n": n, "n_valid": nv, "ms": round(ms, 4),
+                      "candidates_after_2_passes": int(cnt), "median": float(out.item()),
+                      "torch_lower_median": ref}))
+
+
+if __name__ == "__main__":
+    main()
