@@ -116,7 +116,33 @@ def test_workspace_sizes():
     K = 10 + 5 * D + D * (D + 1) // 2 + 2
     assert L.acm_normal_equations_workspace_size(2, 10_000_000) == (2048 + 1) * K * 8
     assert L.acm_reprojection_stats_workspace_size(1000) >= 1000 * 8
-    assert L.acm_median_workspace_size(10) > 0
+    assert L.acm_median_workspace_size(10) >= 10 * 8  # candidate buffer sized for n
+
+
+def test_tuning_knobs_validate_and_restore():
+    """acm_set_tuning (benchmark A/B knobs, results identical for every
+    setting) rejects out-of-range values and returns the previous value."""
+    from apex_camera_models import _lib
+    L = _lib.load()
+    cases = {_lib.TUNE_PROJECT_VARIANT: ([-1, 0, 1, 2, 3, 4, 5, 6, 7], [-2, 8]),
+             _lib.TUNE_RESIDUAL_NT: ([-1, 0, 1], [2]),
+             _lib.TUNE_NE_WAVES: ([0, 1, 3, 4], [2, 5]),
+             _lib.TUNE_FOV_UNROLL: ([1, 2, 4], [3]),
+             _lib.TUNE_NE_UNROLL: ([0, 1, 2], [4]),
+             _lib.TUNE_ALIGN_J: ([-1, 0, 1], [2]),
+             _lib.TUNE_NT_LOADS: ([-1, 0, 1], [2]),
+             _lib.TUNE_NT_LOADS_UNPROJECT: ([-1, 0, 1], [2])}
+    for key, (good, bad) in cases.items():
+        first = L.acm_set_tuning(key, good[0])
+        assert first >= -1, key
+        prev = good[0]
+        for v in good[1:]:
+            assert L.acm_set_tuning(key, v) == prev, (key, v)
+            prev = v
+        for v in bad:
+            assert L.acm_set_tuning(key, v) == _lib.ERR_INVALID_ARGUMENT, (key, v)
+        assert L.acm_set_tuning(key, first) == prev  # a rejected value changed nothing
+    assert L.acm_set_tuning(99, 0) == _lib.ERR_INVALID_ARGUMENT
 
 
 def test_newton_tolerance_threshold_is_exact():
