@@ -573,6 +573,25 @@ static int resident_blocks(const void* kernel) {
     return r;
 }
 
+// Compute units of the current device (cached per device).
+static int cu_count() {
+    static std::mutex mu;
+    static std::map<int, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return it->second;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0) {
+        (void)hipGetLastError();
+        return 256;
+    }
+    cache[dev] = cus;
+    return cus;
+}
+
 // WAVES: minimum waves per SIMD the register allocator must allow
 // (amdgpu_waves_per_eu).  1 leaves it free (KB lands at 176 VGPRs = 2 waves);
 // 3 fits KB in 168 without spills; 4 forces 128 with scratch spills for KB and
@@ -724,9 +743,10 @@ __global__ void k_ne_expand(const double* __restrict__ s, double* __restrict__ o
 }
 
 // ----------------------------------------------------- reprojection stats
+constexpr int kReprojU = 4;
 // pass 1: e_i = ||proj(p_i) - uv_i|| (NaN if the projection fails);
 // per-block [sum e, sum e^2, min, max, count]
-template <class TagT, int LAYOUT>
+template <class TagT, int LAYOUT, bool NTL>
 __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t n,
                                                          const double* __restrict__ pts,
                                                          const double* __restrict__ obs,
@@ -735,24 +755,42 @@ __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t 
     using M = typename TagT::template type<double>;
     const Cam<double> c = make_cam<double>(cam);
     double s = 0.0, ss = 0.0, mn = INFINITY, mx = -INFINITY, cnt = 0.0;
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        double x, y, z;
-        load_point<LAYOUT>(pts, n, i, x, y, z);
-        const double2 o = *reinterpret_cast<const double2*>(obs + 2 * i);
-        double u, v;
-        const uint8_t st = M::template project<false>(c, x, y, z, u, v, nullptr, nullptr);
-        double e = __builtin_nan("");
-        if (st == ST_OK) {
-            const double du = u - o.x, dv = v - o.y;
-            e = sqrt(du * du + dv * dv);
-            s += e;
-            ss += e * e;
-            mn = fmin(mn, e);
-            mx = fmax(mx, e);
-            cnt += 1.0;
+    // each wave streams contiguous chunks of kReprojU x 64 points
+    const size_t nw = (size_t)gridDim.x * (kBlock / 64);
+    constexpr size_t C = (size_t)kReprojU * 64;
+    for (size_t b0 = ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * C; b0 < n;
+         b0 += nw * C) {
+        double x[kReprojU], y[kReprojU], z[kReprojU];
+        double2 o[kReprojU];
+#pragma unroll
+        for (int k = 0; k < kReprojU; ++k) {
+            const size_t i = b0 + k * 64 + (threadIdx.x & 63);
+            x[k] = 0.0; y[k] = 0.0; z[k] = 1.0;
+            o[k] = make_double2(0.0, 0.0);
+            if (i < n) {
+                load_point<LAYOUT, NTL>(pts, n, i, x[k], y[k], z[k]);
+                o[k] = ld2<NTL>(obs + 2 * i);
+            }
         }
-        errs[i] = e;
+#pragma unroll
+        for (int k = 0; k < kReprojU; ++k) {
+            const size_t i = b0 + k * 64 + (threadIdx.x & 63);
+            if (i >= n) break;
+            double u, v;
+            const uint8_t st = M::template project<false>(c, x[k], y[k], z[k], u, v, nullptr,
+                                                          nullptr);
+            double e = __builtin_nan("");
+            if (st == ST_OK) {
+                const double du = u - o[k].x, dv = v - o[k].y;
+                e = sqrt(du * du + dv * dv);
+                s += e;
+                ss += e * e;
+                mn = fmin(mn, e);
+                mx = fmax(mx, e);
+                cnt += 1.0;
+            }
+            errs[i] = e;
+        }
     }
     // sums
     __shared__ double sm[kBlock / 64][5];
@@ -813,17 +851,28 @@ __global__ __launch_bounds__(kBlock) void k_reproj_finish1(const double* __restr
 }
 
 // pass 2: per-block sum (e - mean)^2 over valid errors (error_metrics.rs:92)
+template <bool NTL>
 __global__ __launch_bounds__(kBlock) void k_reproj_pass2(size_t n, const double* __restrict__ errs,
                                                          const double* __restrict__ tot,
                                                          double* __restrict__ parts) {
     const double mean = tot[0] / tot[4];
     double acc[1] = {0.0};
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        const double e = errs[i];
-        if (e == e) {
-            const double d = e - mean;
-            acc[0] += d * d;
+    const size_t nw = (size_t)gridDim.x * (kBlock / 64);
+    constexpr size_t C = (size_t)kReprojU * 64;
+    for (size_t b0 = ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * C; b0 < n;
+         b0 += nw * C) {
+        double e[kReprojU];
+#pragma unroll
+        for (int k = 0; k < kReprojU; ++k) {
+            const size_t i = b0 + k * 64 + (threadIdx.x & 63);
+            e[k] = i < n ? ld1<NTL>(errs + i) : __builtin_nan("");
+        }
+#pragma unroll
+        for (int k = 0; k < kReprojU; ++k) {
+            if (e[k] == e[k]) {
+                const double d = e[k] - mean;
+                acc[0] += d * d;
+            }
         }
     }
     block_sum_store<1>(acc, parts + blockIdx.x);
@@ -1020,15 +1069,23 @@ __device__ __forceinline__ void sel_count(unsigned int* h, bool pred, unsigned d
     }
 }
 
+// The streaming selection kernels run one 1024-lane workgroup per CU: 16
+// waves x kSelU loads in flight per CU, and only #CU workgroups flushing
+// histogram bins / claiming candidate slots with global atomics (thousands
+// of same-address atomics from 1024 small workgroups serialised: 0.47 ms of
+// a 0.67 ms median, profiles/r01_diag_median.log).
+constexpr int kSelBlock = 1024;
+constexpr int kSelWaves = kSelBlock / 64;
+
 // n_dev != nullptr: the value count lives in device memory (the compacted
 // candidate buffer of the later passes).
-template <bool AGG>
-__global__ __launch_bounds__(kBlock) void k_sel_hist(size_t n, const unsigned long long* n_dev,
-                                                     const double* __restrict__ vals,
-                                                     const SelState* __restrict__ st, int pass,
-                                                     double* __restrict__ hist) {
+template <bool AGG, bool NTL>
+__global__ __launch_bounds__(kSelBlock) void k_sel_hist(size_t n, const unsigned long long* n_dev,
+                                                        const double* __restrict__ vals,
+                                                        const SelState* __restrict__ st,
+                                                        int pass, double* __restrict__ hist) {
     __shared__ unsigned int h[2][kSelBins];
-    for (int j = threadIdx.x; j < 2 * kSelBins; j += kBlock) (&h[0][0])[j] = 0;
+    for (int j = threadIdx.x; j < 2 * kSelBins; j += kSelBlock) (&h[0][0])[j] = 0;
     __syncthreads();
     if (n_dev) n = (size_t)*n_dev;
     const unsigned long long pa = st[0].prefix, ma = st[0].mask;
@@ -1036,27 +1093,31 @@ __global__ __launch_bounds__(kBlock) void k_sel_hist(size_t n, const unsigned lo
     const bool same = pa == pb && ma == mb;  // one histogram serves both states
     const int shift = sel_shift(pass);
     const unsigned long long dmask = (1ull << sel_width(pass)) - 1;
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    // whole waves iterate together (the AGG ballots need every lane); kSelU
-    // loads in flight per lane
-    for (size_t i0 = (size_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); i0 < n;
-         i0 += kSelU * stride) {
+    // each wave streams contiguous chunks of kSelU x 64 values (a lane's
+    // kSelU loads are 512 B apart, not a grid stride apart: the read probe
+    // lost 25% with stride-separated loads in flight); whole waves iterate
+    // together, as the AGG ballots need every lane
+    const int lane = threadIdx.x & 63;
+    const size_t nw = (size_t)gridDim.x * kSelWaves;
+    constexpr size_t C = (size_t)kSelU * 64;
+    for (size_t b0 = ((size_t)blockIdx.x * kSelWaves + (threadIdx.x >> 6)) * C; b0 < n;
+         b0 += nw * C) {
         unsigned long long bits[kSelU];
 #pragma unroll
         for (int u = 0; u < kSelU; ++u) {
-            const size_t i = i0 + u * stride + (threadIdx.x & 63);
-            bits[u] = i < n ? (unsigned long long)__double_as_longlong(vals[i]) : ~0ull;
+            const size_t i = b0 + u * 64 + lane;
+            bits[u] = i < n ? (unsigned long long)__double_as_longlong(ld1<NTL>(vals + i)) : ~0ull;
         }
 #pragma unroll
         for (int u = 0; u < kSelU; ++u) {
-            const bool in = i0 + u * stride + (threadIdx.x & 63) < n;
+            const bool in = b0 + u * 64 + lane < n;
             const unsigned d = (unsigned)((bits[u] >> shift) & dmask);
             sel_count<AGG>(h[0], in && (bits[u] & ma) == pa, d);
             if (!same) sel_count<AGG>(h[1], in && (bits[u] & mb) == pb, d);
         }
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < kSelBins; j += kBlock) {
+    for (int j = threadIdx.x; j < kSelBins; j += kSelBlock) {
         const unsigned c0 = h[0][j];
         const unsigned c1 = same ? c0 : h[1][j];
         if (c0) atomicAdd(&hist[j], (double)c0);
@@ -1065,46 +1126,74 @@ __global__ __launch_bounds__(kBlock) void k_sel_hist(size_t n, const unsigned lo
 }
 
 // Candidates of either state (values matching its prefix after the first
-// passes) appended to a compact buffer; later passes read only those.  The
-// buffer order depends on scheduling, the selected ranks do not.
-__global__ __launch_bounds__(kBlock) void k_sel_compact(size_t n, const double* __restrict__ vals,
-                                                        const SelState* __restrict__ st,
-                                                        double* __restrict__ cbuf,
-                                                        unsigned long long* __restrict__ count) {
+// passes) appended to a compact buffer; later passes read only those.  Each
+// workgroup stages its candidates in LDS and claims one slot range with a
+// single global atomic (overflow beyond the LDS stage goes straight out,
+// one atomic per wave).  The buffer order depends on scheduling, the
+// selected ranks do not.
+constexpr int kSelStage = 4096;
+template <bool NTL>
+__global__ __launch_bounds__(kSelBlock) void k_sel_compact(size_t n, const double* __restrict__ vals,
+                                                           const SelState* __restrict__ st,
+                                                           double* __restrict__ cbuf,
+                                                           unsigned long long* __restrict__ count) {
+    __shared__ double stage[kSelStage];
+    __shared__ unsigned int staged, filled;
+    __shared__ unsigned long long gbase;
+    if (threadIdx.x == 0) staged = filled = 0;
+    __syncthreads();
     const unsigned long long pa = st[0].prefix, ma = st[0].mask;
     const unsigned long long pb = st[1].prefix, mb = st[1].mask;
-    const size_t stride = (size_t)gridDim.x * kBlock;
     const int lane = threadIdx.x & 63;
-    for (size_t i0 = (size_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); i0 < n;
-         i0 += kSelU * stride) {
+    const unsigned long long below = (1ull << lane) - 1;
+    const size_t nw = (size_t)gridDim.x * kSelWaves;
+    constexpr size_t C = (size_t)kSelU * 64;
+    for (size_t b0 = ((size_t)blockIdx.x * kSelWaves + (threadIdx.x >> 6)) * C; b0 < n;
+         b0 += nw * C) {
         double v[kSelU];
 #pragma unroll
         for (int u = 0; u < kSelU; ++u) {
-            const size_t i = i0 + u * stride + lane;
-            v[u] = i < n ? vals[i] : 0.0;
+            const size_t i = b0 + u * 64 + lane;
+            v[u] = i < n ? ld1<NTL>(vals + i) : 0.0;
         }
-        // one global atomic per wave per kSelU values (a single counter
-        // address: fewer atomics, less serialisation)
         unsigned long long m[kSelU];
         unsigned total = 0;
 #pragma unroll
         for (int u = 0; u < kSelU; ++u) {
-            const bool in = i0 + u * stride + lane < n;
+            const bool in = b0 + u * 64 + lane < n;
             const unsigned long long bits = (unsigned long long)__double_as_longlong(v[u]);
             m[u] = __ballot(in && ((bits & ma) == pa || (bits & mb) == pb));
             total += (unsigned)__popcll(m[u]);
         }
         if (!total) continue;
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(count, (unsigned long long)total);
-        base = __shfl((long long)base, 0, 64);
-        const unsigned long long below = (1ull << lane) - 1;
+        unsigned pos = 0;
+        if (lane == 0) pos = atomicAdd(&staged, total);
+        pos = (unsigned)__shfl((int)pos, 0, 64);
+        if (pos + total <= (unsigned)kSelStage) {
+            if (lane == 0) atomicMax(&filled, pos + total);
 #pragma unroll
-        for (int u = 0; u < kSelU; ++u) {
-            if ((m[u] >> lane) & 1ull) cbuf[base + __popcll(m[u] & below)] = v[u];
-            base += (unsigned long long)__popcll(m[u]);
+            for (int u = 0; u < kSelU; ++u) {
+                if ((m[u] >> lane) & 1ull) stage[pos + __popcll(m[u] & below)] = v[u];
+                pos += (unsigned)__popcll(m[u]);
+            }
+        } else {  // stage full: this wave's candidates go straight to global
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(count, (unsigned long long)total);
+            base = __shfl((long long)base, 0, 64);
+#pragma unroll
+            for (int u = 0; u < kSelU; ++u) {
+                if ((m[u] >> lane) & 1ull) cbuf[base + __popcll(m[u] & below)] = v[u];
+                base += (unsigned long long)__popcll(m[u]);
+            }
         }
     }
+    __syncthreads();
+    // claims are handed out in order, so the claims that fit the stage are
+    // exactly the prefix [0, filled): later (overflowing) claims went global
+    const unsigned k = filled;
+    if (threadIdx.x == 0 && k) gbase = atomicAdd(count, (unsigned long long)k);
+    __syncthreads();
+    for (unsigned j = threadIdx.x; j < k; j += kSelBlock) cbuf[gbase + j] = stage[j];
 }
 
 // Picks this pass's digit for both states from the (all-reduced) histograms
@@ -1890,12 +1979,14 @@ ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double
     double* tot = p1 + (size_t)nb_max * 5;
     double* p2 = tot + 5;
     double* var = p2 + nb_max;
-    const int nb2 = std::min(nb_max, resident_blocks(reinterpret_cast<const void*>(k_reproj_pass2)));
+    const bool ntl = g_nt_loads != 0;
+    const int nb2 = std::min(nb_max, resident_blocks(reinterpret_cast<const void*>(k_reproj_pass2<true>)));
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
         int nb1 = nb_max;
         auto go = [&](auto lay_c) {
-            auto kern = k_reproj_pass1<TagT, decltype(lay_c)::value>;
+            auto kern = ntl ? k_reproj_pass1<TagT, decltype(lay_c)::value, true>
+                            : k_reproj_pass1<TagT, decltype(lay_c)::value, false>;
             nb1 = std::min(nb1, resident_blocks(reinterpret_cast<const void*>(kern)));
             hipLaunchKernelGGL(kern, dim3(nb1), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
                                points_2d, errs, p1);
@@ -1903,7 +1994,8 @@ ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double
         if (layout == ACM_LAYOUT_AOS) go(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else go(std::integral_constant<int, ACM_LAYOUT_SOA>{});
         hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb1, tot);
-        hipLaunchKernelGGL(k_reproj_pass2, dim3(nb2), dim3(kBlock), 0, s, n, errs, tot, p2);
+        hipLaunchKernelGGL((ntl ? k_reproj_pass2<true> : k_reproj_pass2<false>), dim3(nb2),
+                           dim3(kBlock), 0, s, n, errs, tot, p2);
         hipLaunchKernelGGL(k_sum_columns, dim3(1), dim3(kBlock), 0, s, p2, nb2, 1, var);
         hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, var, result);
         return check_launch("acm_reprojection_stats");
@@ -2122,10 +2214,10 @@ ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
     double* hist = (double*)(st + 2);
     unsigned long long* count = (unsigned long long*)(hist + 2 * kSelBins);
     double* cbuf = (double*)(count + 2);
-    // <= 1024 workgroups: each flushes its non-empty bins with f64 atomics
-    const unsigned nb = (unsigned)std::min(
-        std::min(ne_blocks(n), 1024),
-        resident_blocks(reinterpret_cast<const void*>(k_sel_hist<true>)));
+    // one 1024-lane workgroup per CU (fewer for small n)
+    const unsigned nb = (unsigned)std::max<size_t>(
+        1, std::min<size_t>((size_t)cu_count(), (n + kSelBlock * kSelU - 1) / (kSelBlock * kSelU)));
+    const bool ntl = g_nt_loads != 0;
     // passes 0-1 read every value (pass 0 aggregates its exponent digits per
     // wave); then the candidates sharing either state's 22-bit prefix are
     // compacted and passes 2-5 read only them.
@@ -2134,17 +2226,18 @@ ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
                        (unsigned long long)n_valid, hist, count);
     for (int pass = 0; pass < kSelPasses; ++pass) {
         if (pass == kFullPasses)
-            hipLaunchKernelGGL(k_sel_compact, dim3(nb), dim3(kBlock), 0, s, n, values, st, cbuf,
-                               count);
+            hipLaunchKernelGGL((ntl ? k_sel_compact<true> : k_sel_compact<false>), dim3(nb),
+                               dim3(kSelBlock), 0, s, n, values, st, cbuf, count);
         if (pass == 0)
-            hipLaunchKernelGGL(k_sel_hist<true>, dim3(nb), dim3(kBlock), 0, s, n, nullptr, values,
-                               st, pass, hist);
+            hipLaunchKernelGGL((ntl ? k_sel_hist<true, true> : k_sel_hist<true, false>), dim3(nb),
+                               dim3(kSelBlock), 0, s, n, nullptr, values, st, pass, hist);
         else if (pass < kFullPasses)
-            hipLaunchKernelGGL(k_sel_hist<false>, dim3(nb), dim3(kBlock), 0, s, n, nullptr,
-                               values, st, pass, hist);
+            hipLaunchKernelGGL((ntl ? k_sel_hist<false, true> : k_sel_hist<false, false>),
+                               dim3(nb), dim3(kSelBlock), 0, s, n, nullptr, values, st, pass,
+                               hist);
         else
-            hipLaunchKernelGGL(k_sel_hist<false>, dim3(std::min(nb, 256u)), dim3(kBlock), 0, s,
-                               (size_t)0, count, cbuf, st, pass, hist);
+            hipLaunchKernelGGL((k_sel_hist<false, false>), dim3(nb), dim3(kSelBlock),
+                               0, s, (size_t)0, count, cbuf, st, pass, hist);
         if (allreduce) {  // every rank then picks the same digits
             int rc = check_launch("acm_median_valid (histogram)");
             if (rc) return rc;

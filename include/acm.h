@@ -369,8 +369,8 @@ ACM_API int acm_stream_synchronize(void *stream);
  * acm_residual_jacobian: -1 = auto (default) = line-aligned store windows
  * through LDS, 0 = one point per lane with direct stores, 1 = aligned.
  * ACM_TUNE_NT_LOADS: non-temporal loads of the point / observation streams
- * in the normal-equations kernel (-1 = auto = on, 0, 1; 1 also turns them
- * on in the direct project kernel).  ACM_TUNE_NT_LOADS_UNPROJECT: the same
+ * in the normal-equations, reprojection-statistics and median kernels
+ * (-1 = auto = on, 0, 1; 1 also turns them on in the direct project kernel).  ACM_TUNE_NT_LOADS_UNPROJECT: the same
  * for acm_unproject's pixel stream (-1 = auto = off, 0, 1).
  * Returns the previous value or an error. */
 enum {

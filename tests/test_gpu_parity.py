@@ -370,7 +370,7 @@ def _gpu_median(vals):
 
 
 @pytest.mark.parametrize("case", ["odd", "even", "ties", "tie_pair", "nan_mix", "one", "all_nan",
-                                  "denormal", "wide", "zeros", "big"])
+                                  "denormal", "wide", "zeros", "big", "big_ties", "narrow"])
 def test_median_radix_select_exact(case):
     """acm_median_valid (6-pass 11-bit radix select, both ranks at once) is
     the exact median of the non-NaN values, error_metrics.rs:103-111."""
@@ -387,6 +387,11 @@ def test_median_radix_select_exact(case):
         "wide": 10.0 ** rng.uniform(-300, 300, 4097),
         "zeros": np.zeros(64),
         "big": rng.exponential(0.01, 3_000_001),
+        # every value a candidate after two passes: overflows the per-workgroup
+        # LDS stage of the compaction kernel
+        "big_ties": np.concatenate([np.full(2_000_000, 0.25), rng.uniform(0, 1, 1001)]),
+        # 5M values within a few ulps: candidates share 40+ leading bits
+        "narrow": 1.0 + rng.integers(0, 64, 5_000_000) * np.finfo(np.float64).eps,
     }[case]
     got = _gpu_median(v)
     valid = v[~np.isnan(v)]

@@ -32,20 +32,37 @@ def main():
     def med():
         _lib.check(L.acm_median_valid(n, errs.data_ptr(), None, nv, out.data_ptr(),
                                       ws.data_ptr(), ws_b, None))
-    for _ in range(3):
-        med()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        med()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 10
+
+    def stats():
+        util.reprojection_stats(model, xyz, uv, errs)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 10
+
+    cells = {}
+    for _ in range(2):
+        for ntl in (0, 1):
+            L.acm_set_tuning(_lib.TUNE_NT_LOADS, ntl)
+            for k, f in (("median", med), ("reprojection_stats", stats)):
+                key = f"{k}_ntl{ntl}"
+                cells[key] = min(cells.get(key, 1e9), timed(f))
+    L.acm_set_tuning(_lib.TUNE_NT_LOADS, -1)
+    med()
+    ms = cells["median_ntl1"]
     # candidate count lives right after the 2 states + 2 x 2048 histogram
     cnt = ws.view(torch.int64)[(2 * 24) // 8 + 2 * 2048].item()
     ref = float(torch.median(errs[~torch.isnan(errs)]).item())  # lower median
     print(json.dumps({"what": "median", "n": n, "n_valid": nv, "ms": round(ms, 4),
+                      "cells_ms": {k: round(v, 4) for k, v in cells.items()},
                       "candidates_after_2_passes": int(cnt), "median": float(out.item()),
                       "torch_lower_median": ref}))
 
