@@ -682,13 +682,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             if (kPrefetch) { x = xn; y = yn; z = zn; o = on; }
         }
     } else {
+        // each wave streams contiguous chunks of U x 64 points (loads in
+        // flight a grid stride apart cost DRAM locality, tools/hbm_ceiling.py)
         double x[U], y[U], z[U], xn[U], yn[U], zn[U];
         double2 o[U], on[U];
+        const int lane = threadIdx.x & 63;
+        const size_t nw = (size_t)gridDim.x * (kBlock / 64);
+        constexpr size_t C = (size_t)U * 64;
         auto load = [&](size_t base, double (&xs)[U], double (&ys)[U], double (&zs)[U],
                         double2 (&os)[U]) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const size_t j = base + (size_t)u * stride;
+                const size_t j = base + (size_t)u * 64 + lane;
                 xs[u] = 0.0; ys[u] = 0.0; zs[u] = 1.0;
                 os[u] = make_double2(0.0, 0.0);
                 if (j < n) {
@@ -697,13 +702,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                 }
             }
         };
-        if (kPrefetch) load(i, x, y, z, o);
-        for (; i < n; i += (size_t)U * stride) {
-            if (kPrefetch) load(i + (size_t)U * stride, xn, yn, zn, on);
-            else load(i, x, y, z, o);
+        size_t b0 = ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * C;
+        if (kPrefetch) load(b0, x, y, z, o);
+        for (; b0 < n; b0 += nw * C) {
+            if (kPrefetch) load(b0 + nw * C, xn, yn, zn, on);
+            else load(b0, x, y, z, o);
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (u == 0 || i + (size_t)u * stride < n) accumulate(x[u], y[u], z[u], o[u]);
+                if (b0 + (size_t)u * 64 + lane < n) accumulate(x[u], y[u], z[u], o[u]);
             if (kPrefetch) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) { x[u] = xn[u]; y[u] = yn[u]; z[u] = zn[u]; o[u] = on[u]; }
