@@ -164,8 +164,8 @@ static int g_nt_loads = -1;
 // 1): beside the non-temporal ray stores they measured 2-25% slower for
 // every model (profiles/r01_diag_ntl.log).
 static int g_nt_loads_unproject = -1;
-// FOV grid search: points per lane step (1, 2, 4).
-static int g_fov_unroll = 2;
+// FOV grid search: points per lane step (1 = default, 2, 4).
+static int g_fov_unroll = 1;
 // Outputs above this many bytes are stored non-temporally.  Measured at 10M
 // points (profiles/r01_diag_ntl.log): project without J (170 MB out) 0.056 ms
 // nt vs 0.072 plain; a consumer that re-reads a smaller output soon after
@@ -1498,8 +1498,47 @@ constexpr int kFovGrid = ACM_FOV_GRID_SIZE;
 constexpr int kFovBlock = 320;
 constexpr int kFovMaxBlocks = 2048;
 
-// U: points evaluated per step of a lane (independent atan2 chains the
-// scheduler can interleave; the sum still adds them in point order).
+// atan(b) for 0 <= b <= 1: b * P(b^2), P the degree-20 Chebyshev
+// interpolant of atan(sqrt(s))/sqrt(s) on s in [0, 1] (60-digit mpmath fit,
+// tools/fit_atan.py), evaluated as two interleaved Horner chains in s^2 so
+// the dependent FMA depth is 11, not 21.  Max relative error 4.5e-16 against
+// glibc atan over 2e8 arguments (tools/fit_atan.py --check).
+__constant__ double kAtanE[11] = {  // even-index coefficients c0, c2, ..., c20
+        0x1.0000000000000p+0, 0x1.9999999993702p-3, 0x1.c71c716e724e1p-4,
+        0x1.3b135af6a0e88p-4, 0x1.e1b7b5bcacd55p-5, 0x1.82a3c93dd0230p-5,
+        0x1.2b18b9c197546p-5, 0x1.643110da5054fp-6, 0x1.cd48e33ffd1aep-8,
+        0x1.a53135c884a6dp-11, 0x1.a7d4ff1d17f2cp-17};
+__constant__ double kAtanO[10] = {  // odd-index coefficients c1, c3, ..., c19
+        -0x1.5555555555500p-2, -0x1.2492492327bf2p-3, -0x1.745d1099f743ep-4,
+        -0x1.110df7e57b3d8p-4, -0x1.ae4da39abd8c9p-5, -0x1.59180bd7d7b67p-5,
+        -0x1.e69dd6d612131p-6, -0x1.c012fe85b6413p-7, -0x1.6fa050a5cad37p-9,
+        -0x1.328ae5000addbp-13};
+// (coefficients in constant memory: uniform s_loads into SGPRs, used as FMA
+// operands -- as literals they were materialised in 42 VGPRs, which held the
+// grid kernel at 3 waves/SIMD)
+__device__ __forceinline__ double atan01(double b) {
+    const double* E = kAtanE;
+    const double* O = kAtanO;
+    const double s = b * b, s2 = s * s;
+    double pe = E[10], po = O[9];
+#pragma unroll
+    for (int k = 9; k >= 0; --k) pe = fma(pe, s2, E[k]);
+#pragma unroll
+    for (int k = 8; k >= 0; --k) po = fma(po, s2, O[k]);
+    return b * fma(po, s, pe);
+}
+
+// The general (z <= 0, r == 0, non-finite) form with OCML atan2, out of line:
+// it is rare and uniform per point, and inlined its registers cost the grid
+// kernel a wave of occupancy.
+__device__ __noinline__ double fov_rd_general(double tw2, double r, double z, double w,
+                                              double r2, double rd0) {
+    const double atan_wrd = atan2(tw2 * r, z);             // fov.rs:196
+    return r2 < kEpsSqrt ? rd0 : atan_wrd / (r * w);       // :200-205
+}
+
+// U: points evaluated per step of a lane (independent chains the scheduler
+// can interleave; the sum still adds them in point order).
 template <int LAYOUT, int U>
 __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n, size_t chunk,
                                                         const double* __restrict__ pts,
@@ -1507,7 +1546,9 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n
                                                         const double* __restrict__ table,
                                                         double* __restrict__ parts) {
     __shared__ double sx[kFovBlock], sy[kFovBlock], sz[kFovBlock], su[kFovBlock],
-        sv[kFovBlock], sr2[kFovBlock], sr[kFovBlock];
+        sv[kFovBlock], sr2[kFovBlock], sr[kFovBlock], stz[kFovBlock], szt[kFovBlock],
+        sir[kFovBlock];
+    __shared__ unsigned char sfast[kFovBlock];
     const int t = threadIdx.x;
     const bool active = t < kFovGrid;
     const double fx = cam.params[0], fy = cam.params[1], cx = cam.params[2], cy = cam.params[3];
@@ -1517,6 +1558,7 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n
         tw2 = table[3 * t + 1];
         rd0 = table[3 * t + 2];
     }
+    const double iw = 1.0 / w, itw2 = 1.0 / tw2;
     const size_t b0 = (size_t)blockIdx.x * chunk;
     const size_t b1 = b0 + chunk < n ? b0 + chunk : n;
     double sum = 0.0, cnt = 0.0;
@@ -1527,16 +1569,33 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n
             double x, y, z;
             load_point<LAYOUT>(pts, n, i, x, y, z);
             const double r2 = x * x + y * y;  // :192-193
+            const double r = sqrt(r2);
             sx[t] = x; sy[t] = y; sz[t] = z;
             su[t] = obs[2 * i]; sv[t] = obs[2 * i + 1];
-            sr2[t] = r2; sr[t] = sqrt(r2);
+            sr2[t] = r2; sr[t] = r;
+            // z > 0, r > 0, both finite: atan2(2 tan(w/2) r, z) = atan(2 tan(w/2) r / z)
+            // from per-point r/z, z/r, 1/r shared by every grid lane
+            const bool fast = z > 0.0 && r > 0.0 && z < INFINITY && r < INFINITY;
+            sfast[t] = fast;
+            stz[t] = fast ? r / z : 0.0;
+            szt[t] = fast ? z / r : 0.0;
+            sir[t] = fast ? 1.0 / r : 0.0;
         }
         __syncthreads();
         const int m = (int)(b1 - base < (size_t)kFovBlock ? b1 - base : (size_t)kFovBlock);
         auto eval = [&](int k) -> double {
             const double x = sx[k], y = sy[k], r2 = sr2[k];
-            const double atan_wrd = atan2(tw2 * sr[k], sz[k]);          // :196
-            const double rd = r2 < kEpsSqrt ? rd0 : atan_wrd / (sr[k] * w);  // :200-205
+            double rd;
+            if (sfast[k]) {  // uniform: every lane reads point k
+                // a = 2 tan(w/2) r / z; atan(a) = pi/2 - atan(1/a) above 1
+                const double a = tw2 * stz[k];
+                const bool big = a > 1.0;
+                const double at = atan01(big ? itw2 * szt[k] : a);
+                const double atan_wrd = big ? 1.5707963267948966 - at : at;      // :196
+                rd = r2 < kEpsSqrt ? rd0 : atan_wrd * sir[k] * iw;                // :200-205
+            } else {
+                rd = fov_rd_general(tw2, sr[k], sz[k], w, r2, rd0);
+            }
             const double mx = x * rd, my = y * rd;
             const double du = (fx * mx + cx) - su[k];
             const double dv = (fy * my + cy) - sv[k];
@@ -1565,13 +1624,23 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n
 }
 
 // Chunk sums combined in block order (deterministic), one lane per column.
+// One workgroup per column: lane l sums chunks l, l + 256, ... and the lanes
+// combine in a fixed tree order (deterministic; a lane per column walking all
+// chunks serially was latency-bound: 0.53 ms).
 __global__ __launch_bounds__(kBlock) void k_fov_finish(const double* __restrict__ parts, int nb,
                                                        double* __restrict__ out) {
-    const int c = blockIdx.x * kBlock + threadIdx.x;
-    if (c >= 2 * kFovGrid) return;
+    const int c = blockIdx.x;
     double s = 0.0;
-    for (int b = 0; b < nb; ++b) s += parts[(size_t)b * (2 * kFovGrid) + c];
-    out[c] = s;
+    for (int b = threadIdx.x; b < nb; b += kBlock) s += parts[(size_t)b * (2 * kFovGrid) + c];
+    __shared__ double sm[kBlock / 64];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < kBlock / 64; ++w) t += sm[w];
+        out[c] = t;
+    }
 }
 
 // ---------------------------------------------------------- undistort_image
@@ -2138,9 +2207,22 @@ ACM_API int acm_linear_system_qr(const acm_camera* cam, size_t n, const double* 
 
 // FOV linear_estimation grid (fov.rs:153-251); the selection is host code
 // in solver.hip (acm_fov_grid_select).
+// Chunks of >= 256 points, at most the workgroups resident at once (a grid
+// of 1.33 rounds left a third of the chip idle for the last round).
 static size_t fov_blocks(size_t n) {
-    size_t nb = (n + kBlock - 1) / kBlock;  // >= 256 points per chunk
-    if (nb > (size_t)kFovMaxBlocks) nb = kFovMaxBlocks;
+    static int cap = 0;
+    if (!cap) {
+        int per_cu = 0;
+        const void* k = reinterpret_cast<const void*>(k_fov_grid<ACM_LAYOUT_AOS, 1>);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kFovBlock, 0) != hipSuccess ||
+            per_cu <= 0) {
+            (void)hipGetLastError();
+            per_cu = 4;
+        }
+        cap = std::min(kFovMaxBlocks, per_cu * cu_count());
+    }
+    size_t nb = (n + kBlock - 1) / kBlock;
+    if (nb > (size_t)cap) nb = cap;
     return nb ? nb : 1;
 }
 
@@ -2190,15 +2272,15 @@ ACM_API int acm_fov_grid_errors(const acm_camera* cam, size_t n, const double* p
     };
     auto by_unroll = [&](auto lay_c) {
         switch (g_fov_unroll) {
-        case 1: go(lay_c, std::integral_constant<int, 1>{}); break;
+        case 2: go(lay_c, std::integral_constant<int, 2>{}); break;
         case 4: go(lay_c, std::integral_constant<int, 4>{}); break;
-        default: go(lay_c, std::integral_constant<int, 2>{}); break;
+        default: go(lay_c, std::integral_constant<int, 1>{}); break;
         }
     };
     if (layout == ACM_LAYOUT_AOS) by_unroll(std::integral_constant<int, ACM_LAYOUT_AOS>{});
     else by_unroll(std::integral_constant<int, ACM_LAYOUT_SOA>{});
-    hipLaunchKernelGGL(k_fov_finish, dim3((2 * kFovGrid + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                       s, parts, (int)nb, grid_sums);
+    hipLaunchKernelGGL(k_fov_finish, dim3(2 * kFovGrid), dim3(kBlock), 0, s, parts, (int)nb,
+                       grid_sums);
     return check_launch("acm_fov_grid_errors");
 }
 

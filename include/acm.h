@@ -363,7 +363,7 @@ ACM_API int acm_stream_synchronize(void *stream);
  * acm_residual_jacobian (-1 auto, 0 off = default, 1 on).  ACM_TUNE_NE_WAVES:
  * minimum waves per SIMD the normal-equations kernel is compiled for
  * (0 = per-model default, 1, 3, 4).  ACM_TUNE_FOV_UNROLL: points per lane step of the FOV
- * grid search (1, 2 = default, 4).  ACM_TUNE_NE_UNROLL: points per lane step
+ * grid search (1 = default, 2, 4).  ACM_TUNE_NE_UNROLL: points per lane step
  * of the normal-equations kernel (0 = per-model default, 1, 2).
  * ACM_TUNE_ALIGN_J: kernel of +Jacobian launches of acm_project /
  * acm_residual_jacobian: -1 = auto (default) = line-aligned store windows

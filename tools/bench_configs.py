@@ -180,7 +180,7 @@ def config_fov(n_target):
             by.setdefault(u, []).append(timed(lambda: m.linear_estimation(xyz, uv), reps=3,
                                               warm=1))
             by.setdefault(("w", u), []).append(m.w)
-    L.acm_set_tuning(_lib.TUNE_FOV_UNROLL, 2)
+    L.acm_set_tuning(_lib.TUNE_FOV_UNROLL, 1)
     assert len({v[0] for k, v in by.items() if isinstance(k, tuple)}) == 1
     ms = min(min(by[u]) for u in (1, 2, 4))
     emit({"config": "fov", "what": "FOV grid unroll A/B",
