@@ -1498,36 +1498,6 @@ constexpr int kFovGrid = ACM_FOV_GRID_SIZE;
 constexpr int kFovBlock = 320;
 constexpr int kFovMaxBlocks = 2048;
 
-// atan(b) for 0 <= b <= 1: b * P(b^2), P the degree-20 Chebyshev
-// interpolant of atan(sqrt(s))/sqrt(s) on s in [0, 1] (60-digit mpmath fit,
-// tools/fit_atan.py), evaluated as two interleaved Horner chains in s^2 so
-// the dependent FMA depth is 11, not 21.  Max relative error 4.5e-16 against
-// glibc atan over 2e8 arguments (tools/fit_atan.py --check).
-__constant__ double kAtanE[11] = {  // even-index coefficients c0, c2, ..., c20
-        0x1.0000000000000p+0, 0x1.9999999993702p-3, 0x1.c71c716e724e1p-4,
-        0x1.3b135af6a0e88p-4, 0x1.e1b7b5bcacd55p-5, 0x1.82a3c93dd0230p-5,
-        0x1.2b18b9c197546p-5, 0x1.643110da5054fp-6, 0x1.cd48e33ffd1aep-8,
-        0x1.a53135c884a6dp-11, 0x1.a7d4ff1d17f2cp-17};
-__constant__ double kAtanO[10] = {  // odd-index coefficients c1, c3, ..., c19
-        -0x1.5555555555500p-2, -0x1.2492492327bf2p-3, -0x1.745d1099f743ep-4,
-        -0x1.110df7e57b3d8p-4, -0x1.ae4da39abd8c9p-5, -0x1.59180bd7d7b67p-5,
-        -0x1.e69dd6d612131p-6, -0x1.c012fe85b6413p-7, -0x1.6fa050a5cad37p-9,
-        -0x1.328ae5000addbp-13};
-// (coefficients in constant memory: uniform s_loads into SGPRs, used as FMA
-// operands -- as literals they were materialised in 42 VGPRs, which held the
-// grid kernel at 3 waves/SIMD)
-__device__ __forceinline__ double atan01(double b) {
-    const double* E = kAtanE;
-    const double* O = kAtanO;
-    const double s = b * b, s2 = s * s;
-    double pe = E[10], po = O[9];
-#pragma unroll
-    for (int k = 9; k >= 0; --k) pe = fma(pe, s2, E[k]);
-#pragma unroll
-    for (int k = 8; k >= 0; --k) po = fma(po, s2, O[k]);
-    return b * fma(po, s, pe);
-}
-
 // The general (z <= 0, r == 0, non-finite) form with OCML atan2, out of line:
 // it is rare and uniform per point, and inlined its registers cost the grid
 // kernel a wave of occupancy.
