@@ -749,7 +749,7 @@ __global__ void k_ne_expand(const double* __restrict__ s, double* __restrict__ o
 }
 
 // ----------------------------------------------------- reprojection stats
-constexpr int kReprojU = 4;
+constexpr int kReprojU = 2;
 // pass 1: e_i = ||proj(p_i) - uv_i|| (NaN if the projection fails);
 // per-block [sum e, sum e^2, min, max, count]
 template <class TagT, int LAYOUT, bool NTL>
