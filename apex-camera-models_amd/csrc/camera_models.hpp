@@ -8,8 +8,9 @@
 // makes the validity masks bit-exact: every threshold test sees the same
 // doubles as the reference.  Divisions and square roots are the IEEE
 // correctly-rounded f64 sequences hipcc emits by default (no -ffast-math).
-// Only atan2/sin/cos/tan (OCML) can differ from glibc by ulps, and no status
-// decision depends on them.
+// Only atan2 (our polynomial, atan2_ge0) and sin/cos (OCML) can differ from
+// glibc by ulps, and no status decision depends on them.  Several divisions
+// by one divisor go through div_shared, bit-identical to dividing each.
 //
 // Status decisions are computed branch-free where possible so a wave does
 // not diverge on the rare failing point; the caller selects outputs.
