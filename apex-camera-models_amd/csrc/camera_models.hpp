@@ -96,6 +96,39 @@ __device__ __forceinline__ double atan2_ge0(double y, double x) {
 }
 __device__ __forceinline__ float atan2_ge0(float y, float x) { return atan2(y, x); }
 
+// sin and cos of theta in [0, 2] (KB's unprojection angle, at most ~pi/2):
+// theta * S(theta^2) and C(theta^2), S and C the degree-10 Chebyshev
+// interpolants of sin(sqrt(s))/sqrt(s) and cos(sqrt(s)) on s in [0, 4]
+// (60-digit mpmath fit, tools/fit_atan.py --sincos): max relative error of
+// sin 3.6e-16, max absolute error of cos 3.3e-16.  Outside [0, 2] (or NaN)
+// OCML's sincos.  Coefficients in constant memory (SGPR operands).
+__constant__ double kSinS[11] = {
+    0x1.0000000000000p+0, -0x1.5555555555555p-3, 0x1.1111111111111p-7,
+    -0x1.a01a01a01a014p-13, 0x1.71de3a556c3f4p-19, -0x1.ae64567f35f76p-26,
+    0x1.6124612f7c108p-33, -0x1.ae7f394959b00p-41, 0x1.952ae9a768f94p-49,
+    -0x1.2eff6f253dc73p-57, 0x1.61fa5d5d95885p-66};
+__constant__ double kCosC[11] = {
+    0x1.0000000000000p+0, -0x1.0000000000000p-1, 0x1.5555555555555p-5,
+    -0x1.6c16c16c16c04p-10, 0x1.a01a01a0196cap-16, -0x1.27e4fb775e7b3p-22,
+    0x1.1eed8eefba3c1p-29, -0x1.939743254b313p-37, 0x1.ae7d04cacc91dp-45,
+    -0x1.67bd0466d94d5p-53, 0x1.ceab379e35c76p-62};
+__device__ __forceinline__ void sincos_0_2(double t, double* sn, double* cs) {
+    if (t >= 0.0 && t <= 2.0) {
+        const double s = t * t;
+        double ps = kSinS[10], pc = kCosC[10];
+#pragma unroll
+        for (int k = 9; k >= 0; --k) {
+            ps = fma(ps, s, kSinS[k]);
+            pc = fma(pc, s, kCosC[k]);
+        }
+        *sn = t * ps;
+        *cs = pc;
+        return;
+    }
+    sincos(t, sn, cs);
+}
+__device__ __forceinline__ void sincos_0_2(float t, float* sn, float* cs) { sincosf(t, sn, cs); }
+
 // ------------------------------------------- division by a shared divisor
 // RN(a / b) from y = RN(1 / b) (one IEEE division) and two FMAs: q = RN(a*y)
 // is within one ulp of a/b, so r = a - b*q is exact, and RN(q + r*y) =
@@ -371,7 +404,7 @@ struct KannalaBrandt {
         T xc = small ? T(0) : c2[0];
         T yc = small ? T(0) : c2[1];
         T s, co;
-        sincos(theta, &s, &co);  // one OCML range reduction for both
+        sincos_0_2(theta, &s, &co);  // polynomial on [0, 2], OCML sincos beyond
         T px = s * xc, py = s * yc;
         T n = sqrt(px * px + py * py + co * co);
         const T nq[3] = {px, py, co};

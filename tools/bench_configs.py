@@ -245,6 +245,8 @@ def config5(n_cells):
     from apex_camera_models import KannalaBrandtModel, Resolution, conversion, samples, util
     kp, (w, h) = samples.SAMPLES[2]
     src = KannalaBrandtModel._from_params(kp, Resolution(w, h))
+    uv, xyz = util.sample_points(src, n_cells)  # warm-up: the allocator's first
+    del uv, xyz                                 # multi-GB hipMalloc is not the kernel
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     uv, xyz = util.sample_points(src, n_cells)

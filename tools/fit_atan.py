@@ -6,6 +6,9 @@ computed with 60-digit mpmath, printed as hex floats split into the even
   python tools/fit_atan.py            # print the two coefficient arrays
   python tools/fit_atan.py --check    # + max relative error vs glibc atan
                                       #   (C, fma, 2e8 arguments in [0, 1])
+  python tools/fit_atan.py --sincos   # camera_models.hpp kSinS / kCosC: degree-10
+                                      #   interpolants of sin(sqrt s)/sqrt s, cos(sqrt s)
+                                      #   on s in [0, 4] (theta in [0, 2])
 """
 import os
 import subprocess
@@ -62,7 +65,25 @@ int main(void) {
 """
 
 
+def sincos_coefficients(deg=10):
+    mp.mp.dps = 60
+    n = deg + 1
+    nodes = [(mp.cos(mp.pi * (k + mp.mpf(1) / 2) / n) + 1) * 2 for k in range(n)]  # [0, 4]
+    a = mp.matrix([[x ** j for j in range(n)] for x in nodes])
+
+    def fs(s):
+        return mp.mpf(1) if s == 0 else mp.sin(mp.sqrt(s)) / mp.sqrt(s)
+    cs = mp.lu_solve(a, mp.matrix([fs(x) for x in nodes]))
+    cc = mp.lu_solve(a, mp.matrix([mp.cos(mp.sqrt(x)) for x in nodes]))
+    return [float(cs[j]) for j in range(n)], [float(cc[j]) for j in range(n)]
+
+
 def main():
+    if "--sincos" in sys.argv:
+        s, c = sincos_coefficients()
+        print("S:", ", ".join(v.hex() for v in s))
+        print("C:", ", ".join(v.hex() for v in c))
+        return
     e, o = coefficients()
     print("E:", ", ".join(v.hex() for v in e))
     print("O:", ", ".join(v.hex() for v in o))
