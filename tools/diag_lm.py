@@ -1,0 +1,65 @@
+"""LM loop overhead on config-3 data (KB-sampled correspondences, DS target):
+wall time of acm_lm_optimize vs evaluations x the normal-equation kernel
+time, i.e. the host / launch / copy cost per evaluation.
+
+  python tools/diag_lm.py [--points N]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "apex-camera-models_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=10_000_000)
+    a = ap.parse_args()
+    import torch
+    from apex_camera_models import KannalaBrandtModel, Resolution, conversion, factors, samples
+    from apex_camera_models import util
+    from apex_camera_models.optimizer import (CONVERTER_BOUNDS, LevenbergMarquardt,
+                                              LevenbergMarquardtConfig)
+    kp, (w, h) = samples.SAMPLES[2]
+    src = KannalaBrandtModel._from_params(kp, Resolution(w, h))
+    uv, xyz = util.sample_points(src, a.points)
+    n = xyz.shape[0]
+    base = conversion._init_target("double_sphere", src)
+    base.linear_estimation(xyz, uv)
+    p0 = base.params()
+    f = factors.DoubleSphereCameraParamsFactor(xyz, uv, Resolution(w, h))
+    out = torch.empty((44,), dtype=torch.float64, device="cuda")
+    for _ in range(3):
+        f.normal_equations(p0, out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        f.normal_equations(p0, out)
+    e1.record()
+    torch.cuda.synchronize()
+    ne_ms = e0.elapsed_time(e1) / 20
+    walls, res = [], None
+    for _ in range(4):
+        m = conversion._init_target("double_sphere", src)
+        m._set_params(list(p0))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = LevenbergMarquardt(LevenbergMarquardtConfig()).optimize(
+            m, xyz, uv, bounds=CONVERTER_BOUNDS["double_sphere"])
+        torch.cuda.synchronize()
+        walls.append((time.perf_counter() - t0) * 1e3)
+    wall = min(walls[1:])
+    print(json.dumps({"what": "LM loop overhead", "points": n, "lm_wall_ms": round(wall, 3),
+                      "evaluations": res.evaluations, "iterations": res.iterations,
+                      "ne_ms": round(ne_ms, 4),
+                      "overhead_per_eval_ms": round((wall - res.evaluations * ne_ms)
+                                                    / res.evaluations, 4)}))
+
+
+if __name__ == "__main__":
+    main()
