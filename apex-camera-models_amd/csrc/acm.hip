@@ -1034,7 +1034,8 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(acm_camera cam, Grid g,
 // without a full sort: MSB-first radix select on the f64 bit patterns (for
 // non-negative doubles the unsigned bit order is the numeric order; the NaN
 // markers 0x7ff8.. sort above +inf so they never reach a rank < n_valid).
-// 8 histogram passes of 8 bits per selected rank; state lives on device.
+// The selection state (prefix, mask, remaining rank) of both median ranks
+// lives on device, so the passes need no host round trip.
 struct SelState {
     unsigned long long prefix, mask, k;
 };
