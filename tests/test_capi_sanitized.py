@@ -1,0 +1,45 @@
+"""Host code of libacm under ASan + UBSan, no GPU: acm.hip and solver.hip
+compiled with -Xarch_host -fsanitize=address / -fsanitize=undefined and
+driven by tests/capi_san_driver.cpp through the host-only C-ABI (camera
+init/validation, R-factor merge, k x k SVD solve with the reference's clamps,
+FOV grid selection, sample grid, LM config, tuning keys, workspace sizes).
+About a minute of compilation; GPU sanitizers are not available on the pool."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "apex-camera-models_amd")
+HIPCC = "/opt/rocm/bin/hipcc"
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+
+
+def _compile(src, out):
+    # host side instrumented; device side at -O0 only to keep the build short
+    # (no kernel is launched: the driver exercises host code alone)
+    return subprocess.Popen([HIPCC, "--offload-arch=gfx950", "-O1", "-std=c++17",
+                             "-ffp-contract=off", "-fPIC", "-Xarch_host", "-g", "-Xarch_host",
+                             "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+                             "-Xarch_device", "-O0", "-I", os.path.join(ROOT, "include"), "-c",
+                             os.path.join(PKG, "csrc", src), "-o", out])
+
+
+@pytest.mark.skipif(not (os.path.exists(HIPCC) and os.path.exists(CLANG)), reason="no ROCm")
+def test_host_c_abi_is_clean_under_asan_ubsan(tmp_path):
+    objs = [str(tmp_path / "acm_san.o"), str(tmp_path / "solver_san.o")]
+    procs = [_compile("acm.hip", objs[0]), _compile("solver.hip", objs[1])]
+    assert [p.wait(timeout=600) for p in procs] == [0, 0]
+    exe = str(tmp_path / "capi_san")
+    subprocess.run([CLANG, "-g", "-std=c++17", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "capi_san_driver.cpp"), *objs,
+                    "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lamdhip64", "-o", exe],
+                   check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert r.stdout.startswith("ok"), r.stdout
+    assert "runtime error" not in r.stderr, r.stderr[-4000:]
