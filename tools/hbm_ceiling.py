@@ -30,6 +30,7 @@ def main():
     vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     L.acm_probe_read.argtypes = [vp, sz, vp, ci, ci, ci, vp]
     L.acm_probe_write.argtypes = [vp, sz, ci, vp]
+    L.acm_probe_read_pts.argtypes = [vp, vp, sz, vp, ci, ci, vp]
     L.acm_probe_mimic.argtypes = [sz, vp, vp, vp, vp, ci, ci, ci, vp]
     sh = torch.cuda.current_stream().cuda_stream
     n = a.points
@@ -67,6 +68,13 @@ def main():
                          lambda: L.acm_probe_read(buf.data_ptr(), nb, acc.data_ptr(), g, un, nt,
                                                   sh), nb)
         del buf
+    pts = torch.ones((5 * n,), dtype=torch.float64, device="cuda")  # xyz, then obs
+    for g in (cus * 4, cus * 8, cus * 16):
+        for stage in (0, 1):
+            cell(f"read_pts_aos_grid{g}_{'staged' if stage else 'strided'}_nt",
+                 lambda: L.acm_probe_read_pts(pts.data_ptr(), pts.data_ptr() + 24 * n, n,
+                                              acc.data_ptr(), g, stage, sh), 40 * n)
+    del pts
     wb = 169 * n
     buf = torch.empty((wb // 8,), dtype=torch.float64, device="cuda")
     for nt in (0, 1):

@@ -3,6 +3,8 @@
 //
 //   acm_probe_read   : grid-stride sum of a buffer (the normal-equations
 //                      kernel's pure 40 B/pt read stream, no math)
+//   acm_probe_read_pts: the same stream in its real shape (AoS xyz + 16-B
+//                      observations), per-lane strided or LDS-staged loads
 //   acm_probe_write  : fill a buffer with 16-B stores (plain or nt)
 //   acm_probe_mimic  : the exact traffic of k_project<*, J>: read 24 B/pt
 //                      (AoS xyz), write 16 B uv + 1 B status + `cols` 16-B
@@ -44,6 +46,48 @@ __global__ __launch_bounds__(256) void k_read(const dbl2* __restrict__ p, size_t
     for (; i < n2; i += stride) { const dbl2 a = p[i]; s += a.x + a.y; }
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
     if ((threadIdx.x & 63) == 0) out[(size_t)blockIdx.x * 4 + (threadIdx.x >> 6)] = s;
+}
+
+// The normal-equations read stream with no math: AoS xyz (24 B/pt) + 16-B
+// observations, one 64-point chunk per wave step.  STAGE = 0: three 8-B loads
+// per lane at a 24-B stride; STAGE = 1: the chunk's 1536 B as three dense
+// 512-B wave loads, redistributed through LDS.
+template <bool STAGE>
+__global__ __launch_bounds__(256) void k_read_pts(const double* __restrict__ xyz,
+                                                  const double* __restrict__ obs, size_t n,
+                                                  double* __restrict__ out) {
+    __shared__ double st[4][192];
+    double s = 0.0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const size_t nw = (size_t)gridDim.x * 4;
+    for (size_t b = ((size_t)blockIdx.x * 4 + w) * 64; b < n; b += nw * 64) {
+        const size_t i = b + lane;
+        double x = 0.0, y = 0.0, z = 0.0;
+        if (STAGE && b + 64 <= n) {
+            const double* src = xyz + 3 * b + lane;
+            const double d0 = __builtin_nontemporal_load(src);
+            const double d1 = __builtin_nontemporal_load(src + 64);
+            const double d2 = __builtin_nontemporal_load(src + 128);
+            st[w][lane] = d0;
+            st[w][64 + lane] = d1;
+            st[w][128 + lane] = d2;
+            __builtin_amdgcn_wave_barrier();
+            x = st[w][3 * lane];
+            y = st[w][3 * lane + 1];
+            z = st[w][3 * lane + 2];
+            __builtin_amdgcn_wave_barrier();
+        } else if (i < n) {
+            x = __builtin_nontemporal_load(xyz + 3 * i);
+            y = __builtin_nontemporal_load(xyz + 3 * i + 1);
+            z = __builtin_nontemporal_load(xyz + 3 * i + 2);
+        }
+        if (i < n) {
+            const dbl2 o = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(obs) + i);
+            s += x + y + z + o.x + o.y;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) out[(size_t)blockIdx.x * 4 + w] = s;
 }
 
 template <bool NT>
@@ -91,6 +135,16 @@ int acm_probe_read(const void* buf, size_t bytes, double* out, int grid, int unr
     RD(1) RD(2) RD(4) RD(8)
 #undef RD
     return -1;
+}
+
+// xyz: n AoS points (16-B aligned), obs: n 16-B observations
+int acm_probe_read_pts(const double* xyz, const double* obs, size_t n, double* out, int grid,
+                       int stage, void* stream) {
+    if (stage) hipLaunchKernelGGL(k_read_pts<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                                  xyz, obs, n, out);
+    else hipLaunchKernelGGL(k_read_pts<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, xyz,
+                            obs, n, out);
+    return (int)hipGetLastError();
 }
 
 int acm_probe_write(void* buf, size_t bytes, int nt, void* stream) {
