@@ -166,6 +166,11 @@ static int g_nt_loads = -1;
 static int g_nt_loads_unproject = -1;
 // FOV grid search: points per lane step (1 = default, 2, 4).
 static int g_fov_unroll = 1;
+// acm_lm_optimize without an all-reduce: the normal-equations epilogue writes
+// its P*P + P + 2 results straight into pinned host memory instead of device
+// memory + a device-to-host copy (-1 = auto = on, 0 = off, 1 = on).
+static int g_lm_host_result = -1;
+int lm_host_result() { return g_lm_host_result != 0; }
 // Outputs above this many bytes are stored non-temporally.  Measured at 10M
 // points (profiles/r01_diag_ntl.log): project without J (170 MB out) 0.056 ms
 // nt vs 0.072 plain; a consumer that re-reads a smaller output soon after
@@ -719,33 +724,79 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     block_sum_store<K>(acc, parts + (size_t)blockIdx.x * K);
 }
 
-// expand the structured sums -> [JtJ full (P*P) | Jtr (P) | 0.5*rr | n_valid]
+// Epilogue of k_normal_eq in one launch (it was a column-sum kernel plus a
+// one-lane expansion kernel, 5.0 + 5.7 us per evaluation on config 3, now
+// 7.2 us; profiles/r01s7_lm_kernel_stats_{before,after}.csv): sum the per-workgroup partials
+// (nb x K, row-major) in a fixed order, then expand the structured sums ->
+// [JtJ full (P*P) | Jtr (P) | 0.5*rr | n_valid], one output per lane.
+// Lane t < R*K owns column t % K of the row group t / K (rows g, g + R, ...:
+// adjacent lanes read adjacent columns of one row); the R group sums of a
+// column are then added in group order by one lane.
+constexpr int kNeFinish = 1024;
 template <int P>
-__global__ void k_ne_expand(const double* __restrict__ s, double* __restrict__ out) {
+__global__ __launch_bounds__(kNeFinish) void k_ne_finish(const double* __restrict__ parts, int nb,
+                                                         double* __restrict__ out) {
     using L = NE<P>;
-    constexpr int D = L::D;
-    if (threadIdx.x != 0) return;
-    for (int q = 0; q < P * P; ++q) out[q] = 0.0;
-    const double nv = s[L::K - 1];
-    auto set = [&](int r, int c, double v) { out[r * P + c] = v; out[c * P + r] = v; };
-    set(0, 0, s[0]);
-    set(0, 2, s[1]);
-    set(1, 1, s[L::B2]);
-    set(1, 3, s[L::B1]);
-    set(2, 2, nv);
-    set(3, 3, nv);
-    for (int k = 0; k < D; ++k) {
-        set(0, 4 + k, s[L::A_DU + k]);
-        set(1, 4 + k, s[L::B_DV + k]);
-        set(2, 4 + k, s[L::DU + k]);
-        set(3, 4 + k, s[L::DV + k]);
+    constexpr int D = L::D, K = L::K;
+    constexpr int R = kNeFinish / K;
+    __shared__ double red[R][K];
+    __shared__ double sm[K];
+    const int t = threadIdx.x;
+    if (t < R * K) {
+        // eight rows in flight per lane (the partials come back from other
+        // XCDs' L2 / MALL: a dependent chain of single loads took 11 us,
+        // this 7 us; 32 predicated loads per round trip measured 10 us)
+        const int k = t % K, g = t / K;
+        double a[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = 0.0;
+        int b = g;
+        for (; b + 7 * R < nb; b += 8 * R) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = parts[(size_t)(b + u * R) * K + k];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] += v[u];
+        }
+        for (; b < nb; b += R) a[0] += parts[(size_t)b * K + k];
+        red[g][k] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     }
-    int t = L::DDB;
-    for (int j = 0; j < D; ++j)
-        for (int k = j; k < D; ++k) set(4 + j, 4 + k, s[t++]);
-    for (int q = 0; q < 4 + D; ++q) out[P * P + q] = s[L::G + q];
-    out[P * P + P] = 0.5 * s[L::K - 2];
-    out[P * P + P + 1] = nv;
+    __syncthreads();
+    if (t < K) {
+        double a = 0.0;
+        for (int g = 0; g < R; ++g) a += red[g][t];
+        sm[t] = a;
+    }
+    __syncthreads();
+    if (t >= P * P + P + 2) return;
+    double v = 0.0;
+    if (t < P * P) {
+        // JtJ(i, j), i <= j: pinhole block (fx fy cx cy) and distortion block
+        const int r = t / P, c = t % P;
+        const int i = r < c ? r : c, j = r < c ? c : r;
+        if (j >= 4) {
+            const int kj = j - 4;
+            if (i == 0) v = sm[L::A_DU + kj];
+            else if (i == 1) v = sm[L::B_DV + kj];
+            else if (i == 2) v = sm[L::DU + kj];
+            else if (i == 3) v = sm[L::DV + kj];
+            else {
+                const int ki = i - 4;  // upper triangle, row-major from (ki, ki)
+                v = sm[L::DDB + ki * D - ki * (ki - 1) / 2 + (kj - ki)];
+            }
+        } else if (i == 0 && j == 0) v = sm[0];
+        else if (i == 0 && j == 2) v = sm[1];
+        else if (i == 1 && j == 1) v = sm[L::B2];
+        else if (i == 1 && j == 3) v = sm[L::B1];
+        else if (i == j) v = sm[K - 1];  // (2, 2), (3, 3): n_valid
+    } else if (t < P * P + P) {
+        v = sm[L::G + (t - P * P)];
+    } else if (t == P * P + P) {
+        v = 0.5 * sm[K - 2];
+    } else {
+        v = sm[K - 1];
+    }
+    out[t] = v;
 }
 
 // ----------------------------------------------------- reprojection stats
@@ -1968,9 +2019,7 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
         using TagT = decltype(tag);
         using M = typename TagT::template type<double>;
         constexpr int P = M::P;
-        constexpr int K = NE<P>::K;
         double* parts = (double*)workspace;
-        double* sums = parts + (size_t)nb_max * K;
         int nb = nb_max;
         using Def = NeDefault<TagT>;
         const int wv = g_ne_waves ? g_ne_waves : Def::W;
@@ -1994,8 +2043,7 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
         };
         if (layout == ACM_LAYOUT_AOS) by_waves(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else by_waves(std::integral_constant<int, ACM_LAYOUT_SOA>{});
-        hipLaunchKernelGGL(k_sum_columns, dim3(K), dim3(kBlock), 0, s, parts, nb, K, sums);
-        hipLaunchKernelGGL(k_ne_expand<P>, dim3(1), dim3(64), 0, s, sums, result);
+        hipLaunchKernelGGL(k_ne_finish<P>, dim3(1), dim3(kNeFinish), 0, s, parts, nb, result);
         return check_launch("acm_normal_equations");
     });
 }
@@ -2415,6 +2463,12 @@ ACM_API int acm_set_tuning(int key, int value) {
         if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
         const int old = g_nt_loads_unproject;
         g_nt_loads_unproject = value;
+        return old;
+    }
+    if (key == ACM_TUNE_LM_HOST_RESULT) {
+        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
+        const int old = g_lm_host_result;
+        g_lm_host_result = value;
         return old;
     }
     if (key == ACM_TUNE_FOV_UNROLL) {

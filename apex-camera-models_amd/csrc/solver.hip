@@ -22,6 +22,7 @@
 
 namespace acm {
 int set_error(int code, const std::string& msg);  // acm.hip (one last-error slot)
+int lm_host_result();                              // acm.hip, ACM_TUNE_LM_HOST_RESULT
 }
 
 namespace {
@@ -328,6 +329,23 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
     const int R = P * P + P + 2;
     hipStream_t s = (hipStream_t)stream;
     std::vector<double> h(R);
+    // Without an all-reduce the epilogue kernel writes the R results straight
+    // into pinned, device-mapped host memory: no device-to-host copy launch
+    // per evaluation (one buffer per host thread, kept for the process).
+    static thread_local double* pinned = nullptr;
+    double* res_out = d_res;
+    if (!allreduce && acm::lm_host_result()) {
+        if (!pinned) {
+            void* p = nullptr;
+            if (hipHostMalloc(&p, 128 * sizeof(double),
+                              hipHostMallocMapped | hipHostMallocPortable |
+                                  hipHostMallocCoherent) == hipSuccess)
+                pinned = (double*)p;
+            else
+                (void)hipGetLastError();
+        }
+        if (pinned) res_out = pinned;
+    }
     acm_lm_summary sum;
     std::memset(&sum, 0, sizeof(sum));
 
@@ -340,15 +358,20 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
         acm_camera c = *cam;
         for (int i = 0; i < P; ++i) c.params[i] = x[i];
         int rc = acm_normal_equations(&c, n, points_3d, layout, points_2d, cfg->invalid_policy,
-                                      d_res, workspace, ne_ws, stream);
+                                      res_out, workspace, ne_ws, stream);
         if (rc) return rc;
         if (allreduce) {
             rc = allreduce(allreduce_ctx, d_res, (size_t)R, stream);
             if (rc) return sfail(ACM_ERR_HIP, "all-reduce callback failed");
         }
-        if (hip_ok(hipMemcpyAsync(h.data(), d_res, R * sizeof(double), hipMemcpyDeviceToHost, s)) ||
-            hip_ok(hipStreamSynchronize(s)))
+        if (res_out != d_res) {
+            if (hip_ok(hipStreamSynchronize(s))) return sfail(ACM_ERR_HIP, "LM: stream failed");
+            std::memcpy(h.data(), res_out, R * sizeof(double));
+        } else if (hip_ok(hipMemcpyAsync(h.data(), d_res, R * sizeof(double),
+                                         hipMemcpyDeviceToHost, s)) ||
+                   hip_ok(hipStreamSynchronize(s))) {
             return sfail(ACM_ERR_HIP, "LM: device copy failed");
+        }
         ++sum.evaluations;
         std::memcpy(A, h.data(), P * P * sizeof(double));
         for (int i = 0; i < P; ++i) g[i] = h[P * P + i];

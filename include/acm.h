@@ -372,6 +372,9 @@ ACM_API int acm_stream_synchronize(void *stream);
  * in the normal-equations, reprojection-statistics and median kernels
  * (-1 = auto = on, 0, 1; 1 also turns them on in the direct project kernel).  ACM_TUNE_NT_LOADS_UNPROJECT: the same
  * for acm_unproject's pixel stream (-1 = auto = off, 0, 1).
+ * ACM_TUNE_LM_HOST_RESULT: acm_lm_optimize without an all-reduce callback
+ * has the normal-equations kernel write its results straight into pinned
+ * host memory rather than device memory plus a copy (-1 = auto = on, 0, 1).
  * Returns the previous value or an error. */
 enum {
     ACM_TUNE_PROJECT_VARIANT = 0,
@@ -381,7 +384,8 @@ enum {
     ACM_TUNE_NE_UNROLL = 4,
     ACM_TUNE_ALIGN_J = 5,
     ACM_TUNE_NT_LOADS = 6,
-    ACM_TUNE_NT_LOADS_UNPROJECT = 7
+    ACM_TUNE_NT_LOADS_UNPROJECT = 7,
+    ACM_TUNE_LM_HOST_RESULT = 8
 };
 ACM_API int acm_set_tuning(int key, int value);
 

@@ -196,6 +196,27 @@ def test_lm_rccl_allreduce_single_rank():
         dist.destroy_process_group()
 
 
+def test_lm_host_result_matches_device_copy():
+    """ACM_TUNE_LM_HOST_RESULT: the epilogue writing the normal equations
+    straight into pinned host memory gives the same LM run, bit for bit, as
+    device memory + a device-to-host copy."""
+    from apex_camera_models import KannalaBrandtModel, Resolution, _lib, conversion, util
+    L = _lib.load()
+    params, (w, h) = SAMPLES[KB]
+    src = KannalaBrandtModel._from_params(params, Resolution(w, h))
+    uv, xyz = util.sample_points(src, 200_000)
+    runs = []
+    try:
+        for v in (0, 1):
+            L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, v)
+            runs.append(conversion.convert(src, "double_sphere", xyz, uv))
+    finally:
+        L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, -1)
+    assert runs[0].model.params() == runs[1].model.params()
+    assert runs[0].lm_iterations == runs[1].lm_iterations
+    assert runs[1].convergence_status == "Converged"
+
+
 # ---------------------------------------------------------------- FOV
 FOV = 6
 
