@@ -481,24 +481,6 @@ __device__ __forceinline__ void block_sum_store(const double (&acc)[K], double* 
     }
 }
 
-// Second pass: column k of `parts` ([nb][K]) summed in a fixed order by one
-// workgroup per k (deterministic).
-__global__ __launch_bounds__(kBlock) void k_sum_columns(const double* __restrict__ parts, int nb,
-                                                        int K, double* __restrict__ out) {
-    const int k = blockIdx.x;
-    double s = 0.0;
-    for (int b = threadIdx.x; b < nb; b += kBlock) s += parts[(size_t)b * K + k];
-    __shared__ double sm[kBlock / 64];
-    s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
-        for (int w = 0; w < kBlock / 64; ++w) t += sm[w];
-        out[k] = t;
-    }
-}
-
 // ---------------------------------------------------- normal equations
 // Every model's Jacobian rows have the same structure (camera_models.hpp):
 //   u-row [a, 0, 1, 0, du_0 .. du_{D-1}],  v-row [0, b, 0, 1, dv_0 .. dv_{D-1}]
@@ -800,10 +782,74 @@ __global__ __launch_bounds__(kNeFinish) void k_ne_finish(const double* __restric
 }
 
 // ----------------------------------------------------- reprojection stats
+// One streaming pass.  The variance is not a second pass over the errors
+// (error_metrics.rs:92 sums (e - mean)^2 after the mean): each lane keeps
+// shifted sums S = sum (e - K), Q = sum (e - K)^2 about its first valid error
+// K, i.e. (count, mean, M2) of its own errors without cancellation (K is a
+// sample of the same distribution), and the lanes / waves / workgroups are
+// merged in a fixed order with Chan's pairwise update
+//   M2 = M2_a + M2_b + d^2 n_a n_b / n,   d = mean_b - mean_a,
+// which equals the two-pass sum of squared deviations up to rounding (the
+// reference's own sums are in a different order anyway).  This drops the
+// 8 B/point re-read of the errors and three small launches.
+struct Mv {
+    double n, m, M2;
+};
+
+__device__ __forceinline__ Mv mv_merge(const Mv& a, const Mv& b) {
+    if (a.n == 0.0) return b;
+    if (b.n == 0.0) return a;
+    const double n = a.n + b.n;
+    const double d = b.m - a.m;
+    return Mv{n, a.m + d * (b.n / n), a.M2 + b.M2 + d * d * (a.n * (b.n / n))};
+}
+
+__device__ __forceinline__ Mv mv_wave(Mv a) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const Mv b{__shfl_xor(a.n, off, 64), __shfl_xor(a.m, off, 64), __shfl_xor(a.M2, off, 64)};
+        a = mv_merge(a, b);
+    }
+    return a;
+}
+
 constexpr int kReprojU = 2;
-// pass 1: e_i = ||proj(p_i) - uv_i|| (NaN if the projection fails);
-// per-block [sum e, sum e^2, min, max, count]
-template <class TagT, int LAYOUT, bool NTL>
+constexpr int kReprojW = 7;  // per-workgroup [sum e, sum e^2, min, max, count, mean, M2]
+
+// [sum, sumsq, min, max, count] + (count, mean, M2) of a wave -> lane 0's
+// values -> sm[wid]; then lane 0 of the workgroup merges the waves in order
+__device__ __forceinline__ void reproj_block_store(double s, double ss, double mn, double mx,
+                                                   Mv v, double* __restrict__ out) {
+    __shared__ double sm[kBlock / 64][kReprojW];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    s = wave_sum(s);
+    ss = wave_sum(ss);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        mn = fmin(mn, __shfl_xor(mn, off, 64));
+        mx = fmax(mx, __shfl_xor(mx, off, 64));
+    }
+    v = mv_wave(v);
+    if (lane == 0) {
+        sm[wid][0] = s; sm[wid][1] = ss; sm[wid][2] = mn; sm[wid][3] = mx;
+        sm[wid][4] = v.n; sm[wid][5] = v.m; sm[wid][6] = v.M2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0, b = 0, m0 = INFINITY, m1 = -INFINITY;
+        Mv t{0.0, 0.0, 0.0};
+        for (int w = 0; w < kBlock / 64; ++w) {
+            a += sm[w][0]; b += sm[w][1]; m0 = fmin(m0, sm[w][2]); m1 = fmax(m1, sm[w][3]);
+            t = mv_merge(t, Mv{sm[w][4], sm[w][5], sm[w][6]});
+        }
+        out[0] = a; out[1] = b; out[2] = m0; out[3] = m1; out[4] = t.n; out[5] = t.m;
+        out[6] = t.M2;
+    }
+}
+
+// e_i = ||proj(p_i) - uv_i|| (NaN if the projection fails); per-workgroup
+// partials (kReprojW doubles).  NTS: non-temporal error stores.
+template <class TagT, int LAYOUT, bool NTL, bool NTS>
 __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t n,
                                                          const double* __restrict__ pts,
                                                          const double* __restrict__ obs,
@@ -812,6 +858,7 @@ __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t 
     using M = typename TagT::template type<double>;
     const Cam<double> c = make_cam<double>(cam);
     double s = 0.0, ss = 0.0, mn = INFINITY, mx = -INFINITY, cnt = 0.0;
+    double K = 0.0, S = 0.0, Q = 0.0;  // shifted sums about this lane's first valid error
     // each wave streams contiguous chunks of kReprojU x 64 points
     const size_t nw = (size_t)gridDim.x * (kBlock / 64);
     constexpr size_t C = (size_t)kReprojU * 64;
@@ -844,108 +891,44 @@ __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t 
                 ss += e * e;
                 mn = fmin(mn, e);
                 mx = fmax(mx, e);
+                K = cnt == 0.0 ? e : K;
+                const double d = e - K;
+                S += d;
+                Q += d * d;
                 cnt += 1.0;
             }
-            errs[i] = e;
+            if (NTS) __builtin_nontemporal_store(e, errs + i);
+            else errs[i] = e;
         }
     }
-    // sums
-    __shared__ double sm[kBlock / 64][5];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    s = wave_sum(s);
-    ss = wave_sum(ss);
-    cnt = wave_sum(cnt);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        mn = fmin(mn, __shfl_xor(mn, off, 64));
-        mx = fmax(mx, __shfl_xor(mx, off, 64));
-    }
-    if (lane == 0) {
-        sm[wid][0] = s; sm[wid][1] = ss; sm[wid][2] = mn; sm[wid][3] = mx; sm[wid][4] = cnt;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double a = 0, b = 0, m0 = INFINITY, m1 = -INFINITY, k = 0;
-        for (int w = 0; w < kBlock / 64; ++w) {
-            a += sm[w][0]; b += sm[w][1]; m0 = fmin(m0, sm[w][2]); m1 = fmax(m1, sm[w][3]);
-            k += sm[w][4];
-        }
-        double* o = parts + (size_t)blockIdx.x * 5;
-        o[0] = a; o[1] = b; o[2] = m0; o[3] = m1; o[4] = k;
-    }
+    const double mloc = cnt > 0.0 ? S / cnt : 0.0;
+    const Mv v{cnt, K + mloc, cnt > 0.0 ? Q - S * mloc : 0.0};
+    reproj_block_store(s, ss, mn, mx, v, parts + (size_t)blockIdx.x * kReprojW);
 }
 
-// fixed-order finish of pass 1: tot = [sum, sumsq, min, max, count]
+// fixed-order finish: tot = [sum, sumsq, min, max, count, mean, M2]
 __global__ __launch_bounds__(kBlock) void k_reproj_finish1(const double* __restrict__ parts,
                                                            int nb, double* __restrict__ tot) {
-    double s = 0, ss = 0, mn = INFINITY, mx = -INFINITY, cnt = 0;
+    double s = 0, ss = 0, mn = INFINITY, mx = -INFINITY;
+    Mv v{0.0, 0.0, 0.0};
     for (int b = threadIdx.x; b < nb; b += kBlock) {
-        const double* p = parts + (size_t)b * 5;
-        s += p[0]; ss += p[1]; mn = fmin(mn, p[2]); mx = fmax(mx, p[3]); cnt += p[4];
+        const double* p = parts + (size_t)b * kReprojW;
+        s += p[0]; ss += p[1]; mn = fmin(mn, p[2]); mx = fmax(mx, p[3]);
+        v = mv_merge(v, Mv{p[4], p[5], p[6]});
     }
-    __shared__ double sm[kBlock / 64][5];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    s = wave_sum(s);
-    ss = wave_sum(ss);
-    cnt = wave_sum(cnt);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        mn = fmin(mn, __shfl_xor(mn, off, 64));
-        mx = fmax(mx, __shfl_xor(mx, off, 64));
-    }
-    if (lane == 0) {
-        sm[wid][0] = s; sm[wid][1] = ss; sm[wid][2] = mn; sm[wid][3] = mx; sm[wid][4] = cnt;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double a = 0, b = 0, m0 = INFINITY, m1 = -INFINITY, k = 0;
-        for (int w = 0; w < kBlock / 64; ++w) {
-            a += sm[w][0]; b += sm[w][1]; m0 = fmin(m0, sm[w][2]); m1 = fmax(m1, sm[w][3]);
-            k += sm[w][4];
-        }
-        tot[0] = a; tot[1] = b; tot[2] = m0; tot[3] = m1; tot[4] = k;
-    }
-}
-
-// pass 2: per-block sum (e - mean)^2 over valid errors (error_metrics.rs:92)
-template <bool NTL>
-__global__ __launch_bounds__(kBlock) void k_reproj_pass2(size_t n, const double* __restrict__ errs,
-                                                         const double* __restrict__ tot,
-                                                         double* __restrict__ parts) {
-    const double mean = tot[0] / tot[4];
-    double acc[1] = {0.0};
-    const size_t nw = (size_t)gridDim.x * (kBlock / 64);
-    constexpr size_t C = (size_t)kReprojU * 64;
-    for (size_t b0 = ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * C; b0 < n;
-         b0 += nw * C) {
-        double e[kReprojU];
-#pragma unroll
-        for (int k = 0; k < kReprojU; ++k) {
-            const size_t i = b0 + k * 64 + (threadIdx.x & 63);
-            e[k] = i < n ? ld1<NTL>(errs + i) : __builtin_nan("");
-        }
-#pragma unroll
-        for (int k = 0; k < kReprojU; ++k) {
-            if (e[k] == e[k]) {
-                const double d = e[k] - mean;
-                acc[0] += d * d;
-            }
-        }
-    }
-    block_sum_store<1>(acc, parts + blockIdx.x);
+    reproj_block_store(s, ss, mn, mx, v, tot);
 }
 
 // result = [rmse, min, max, mean, stddev, n_valid, sum, sumsq]
-__global__ void k_reproj_final(const double* __restrict__ tot, const double* __restrict__ var_sum,
-                               double* __restrict__ out) {
+__global__ void k_reproj_final(const double* __restrict__ tot, double* __restrict__ out) {
     if (threadIdx.x != 0) return;
     const double nn = tot[4];
-    const double mean = tot[0] / nn;
+    const double mean = tot[0] / nn;  // error_metrics.rs:88-89: sum / n
     out[0] = sqrt(tot[1] / nn);
     out[1] = tot[2];
     out[2] = tot[3];
     out[3] = mean;
-    out[4] = sqrt(var_sum[0] / nn);
+    out[4] = sqrt(fmax(tot[6], 0.0) / nn);
     out[5] = nn;
     out[6] = tot[0];
     out[7] = tot[1];
@@ -2049,9 +2032,9 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
 }
 
 ACM_API size_t acm_reprojection_stats_workspace_size(size_t n) {
-    // errors (N) + pass-1 partials (nb*5) + totals (5) + pass-2 partials (nb) + var (1)
+    // errors (N) + per-workgroup partials (nb * 7) + totals (7)
     const size_t nb = (size_t)ne_blocks(n);
-    return (n + nb * 5 + 5 + nb + 1) * sizeof(double);
+    return (n + nb * kReprojW + kReprojW) * sizeof(double);
 }
 
 ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double* points_3d,
@@ -2070,17 +2053,18 @@ ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double
     double* ws = (double*)workspace;
     double* errs = errors ? errors : ws;
     double* p1 = ws + n;
-    double* tot = p1 + (size_t)nb_max * 5;
-    double* p2 = tot + 5;
-    double* var = p2 + nb_max;
+    double* tot = p1 + (size_t)nb_max * kReprojW;
     const bool ntl = g_nt_loads != 0;
-    const int nb2 = std::min(nb_max, resident_blocks(reinterpret_cast<const void*>(k_reproj_pass2<true>)));
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
         int nb1 = nb_max;
+        const bool nts = n * sizeof(double) > kNtThresholdBytes;
         auto go = [&](auto lay_c) {
-            auto kern = ntl ? k_reproj_pass1<TagT, decltype(lay_c)::value, true>
-                            : k_reproj_pass1<TagT, decltype(lay_c)::value, false>;
+            constexpr int LAY = decltype(lay_c)::value;
+            auto kern = ntl ? k_reproj_pass1<TagT, LAY, true, false>
+                            : k_reproj_pass1<TagT, LAY, false, false>;
+            if (nts) kern = ntl ? k_reproj_pass1<TagT, LAY, true, true>
+                                : k_reproj_pass1<TagT, LAY, false, true>;
             nb1 = std::min(nb1, resident_blocks(reinterpret_cast<const void*>(kern)));
             hipLaunchKernelGGL(kern, dim3(nb1), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
                                points_2d, errs, p1);
@@ -2088,10 +2072,7 @@ ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double
         if (layout == ACM_LAYOUT_AOS) go(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else go(std::integral_constant<int, ACM_LAYOUT_SOA>{});
         hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb1, tot);
-        hipLaunchKernelGGL((ntl ? k_reproj_pass2<true> : k_reproj_pass2<false>), dim3(nb2),
-                           dim3(kBlock), 0, s, n, errs, tot, p2);
-        hipLaunchKernelGGL(k_sum_columns, dim3(1), dim3(kBlock), 0, s, p2, nb2, 1, var);
-        hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, var, result);
+        hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, result);
         return check_launch("acm_reprojection_stats");
     });
 }

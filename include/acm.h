@@ -175,7 +175,9 @@ ACM_API int acm_normal_equations(const acm_camera *cam, size_t n,
 /* compute_reprojection_error (error_metrics.rs:62-121) minus the median:
  * result (device, f64): [rmse, min, max, mean, stddev, n_valid, sum, sumsq]
  * errors (nullable, device, N f64): per-point ||proj - obs||, NaN if failed.
- * The stddev uses the reference's two-pass sum((e - mean)^2) / n. */
+ * The stddev is sum((e - mean)^2) / n (the reference's two-pass form)
+ * computed in the same single pass: per-lane shifted sums merged with
+ * Chan's pairwise update (equal up to rounding). */
 ACM_API size_t acm_reprojection_stats_workspace_size(size_t n);
 ACM_API int acm_reprojection_stats(const acm_camera *cam, size_t n,
                                    const double *points_3d, int layout,

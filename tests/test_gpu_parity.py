@@ -223,6 +223,34 @@ def test_reprojection_error_vs_oracle(golden_dir, model):
         assert pe.min == ref["min"] and pe.max == ref["max"] and pe.median == ref["median"]
 
 
+@pytest.mark.parametrize("n", [1, 2, 63, 65, 1000, 300_001])
+def test_reprojection_stddev_single_pass_no_cancellation(n):
+    """The one-pass variance (per-lane shifted sums + Chan merges) against
+    the oracle's two-pass sum((e - mean)^2) where E[e^2] - mean^2 would
+    cancel: errors of ~424 px with a spread of ~1e-3 px (a sum-of-squares
+    formula keeps ~4 digits here).  Ragged n, one point and all-equal cases."""
+    import torch
+    from apex_camera_models import samples, util
+    params, (w, h) = samples.SAMPLES[0]
+    rng = np.random.default_rng(n)
+    xyz = np.stack([rng.uniform(-0.3, 0.3, n), rng.uniform(-0.3, 0.3, n),
+                    rng.uniform(1.0, 2.0, n)], 1)
+    uv0, st0, _ = O.project(0, params, w, h, xyz)
+    m = _model_obj(0, params, w, h)
+    for spread in (1e-3, 0.0):
+        obs = uv0 + 300.0 + spread * np.sin(np.arange(n))[:, None]
+        pe = util.compute_reprojection_error(m, torch.as_tensor(xyz), torch.as_tensor(obs))
+        ref, nv = O.reprojection_error(0, params, w, h, xyz, obs)
+        assert pe.n_valid == nv
+        assert abs(pe.mean - ref["mean"]) <= TOL * ref["mean"]
+        # stddev to 1e-9 of itself, or -- when the spread is 0 -- to the
+        # rounding of the oracle's own sequential mean (n eps mean), which
+        # then is all its two-pass stddev measures
+        slack = 4.0 * n * np.finfo(float).eps * ref["mean"]
+        assert abs(pe.stddev - ref["stddev"]) <= 1e-9 * ref["stddev"] + slack, \
+            (spread, pe.stddev, ref["stddev"])
+
+
 def test_reprojection_error_zero_points():
     import torch
     from apex_camera_models import util
