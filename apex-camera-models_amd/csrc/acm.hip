@@ -166,6 +166,10 @@ static int g_nt_loads = -1;
 static int g_nt_loads_unproject = -1;
 // FOV grid search: points per lane step (1 = default, 2, 4).
 static int g_fov_unroll = 1;
+// sample_points: -1 = auto = single pass with decoupled look-back and the
+// per-model tile (SampleR), 0 = the two-pass count / scan / write path,
+// 1 / 2 / 3 = single pass with tiles of 4 / 8 / 16 x 256 cells.
+static int g_sample_fused = -1;
 // acm_lm_optimize without an all-reduce: the normal-equations epilogue writes
 // its P*P + P + 2 results straight into pinned host memory instead of device
 // memory + a device-to-host copy (-1 = auto = on, 0 = off, 1 = on).
@@ -1060,6 +1064,123 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(acm_camera cam, Grid g,
         }
         run += tot;
         __syncthreads();  // sm is rewritten next round
+    }
+}
+
+// Single pass (ACM_TUNE_SAMPLE_FUSED, default): each workgroup takes the
+// next tile of kFusedR x 256 cells from an atomic ticket, unprojects them
+// once keeping the rays in registers, publishes its kept count, and finds
+// its output offset by a decoupled look-back over the tiles before it (one
+// status word per tile: flag in bits 62-63 -- 1 = count of this tile only,
+// 2 = inclusive prefix -- and the count below).  Wave 0 inspects 64
+// predecessors per load.  The ticket order makes every predecessor a
+// workgroup that is already running, and a running workgroup publishes its
+// count without waiting on anything, so the look-back always terminates.
+// The kept points come out in cell order exactly as from the two-pass path.
+constexpr int kFusedRMin = 4;  // smallest tile (rounds of 256 cells) any setting uses
+// Per-model tile: fewer, larger tiles mean fewer same-address ticket atomics
+// and look-backs, more rays held in registers.  Fastest cell of the
+// interleaved {4, 8, 16} x 256 sweep at 1e8 cells (profiles/r01s7_diag_sample.log).
+template <class TagT> struct SampleR { static constexpr int R = 8; };
+template <> struct SampleR<Tag<Pinhole>> { static constexpr int R = 16; };
+template <> struct SampleR<Tag<Ucm>> { static constexpr int R = 16; };
+template <> struct SampleR<Tag<Eucm>> { static constexpr int R = 16; };
+constexpr size_t kFusedCells = (size_t)kBlock * kFusedRMin;
+constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
+
+template <class TagT, int kFusedR>
+__global__ __launch_bounds__(kBlock) void k_sample_fused(acm_camera cam, Grid g, size_t cells,
+                                                         uint64_t* __restrict__ ticket,
+                                                         uint64_t* __restrict__ status,
+                                                         double* __restrict__ uv_out,
+                                                         double* __restrict__ xyz_out,
+                                                         uint64_t* __restrict__ out_counts) {
+    const Cam<double> c = make_cam<double>(cam);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ uint64_t s_tile, s_excl;
+    __shared__ uint32_t sm[kFusedR][kBlock / 64];
+    if (threadIdx.x == 0) s_tile = atomicAdd((unsigned long long*)ticket, 1ull);
+    __syncthreads();
+    const uint64_t tile = s_tile;
+    constexpr size_t kTile = (size_t)kBlock * kFusedR;
+    const size_t base = (size_t)tile * kTile;
+    double X[kFusedR], Y[kFusedR], Z[kFusedR];
+    uint64_t m[kFusedR];
+#pragma unroll
+    for (int r = 0; r < kFusedR; ++r) {
+        const size_t cell = base + (size_t)r * kBlock + threadIdx.x;
+        bool keep = false;
+        double u, v;
+        X[r] = Y[r] = Z[r] = 0.0;
+        if (cell < cells) keep = sample_cell<TagT>(c, g, cell, u, v, X[r], Y[r], Z[r]);
+        m[r] = __ballot(keep);
+        if (lane == 0) sm[r][wid] = (uint32_t)__popcll(m[r]);
+    }
+    __syncthreads();
+    if (wid == 0) {
+        uint64_t agg = 0;
+        for (int r = 0; r < kFusedR; ++r)
+            for (int w = 0; w < kBlock / 64; ++w) agg += sm[r][w];
+        if (lane == 0)
+            __hip_atomic_store(status + tile, (tile == 0 ? kLbIncl : kLbAgg) | agg,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t excl = 0;
+        if (tile > 0) {
+            int64_t top = (int64_t)tile - 1;  // lane l inspects tile top - l
+            for (;;) {
+                const int64_t idx = top - lane;
+                const uint64_t w = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT)
+                                            : kLbIncl;  // before tile 0: prefix 0
+                const uint64_t incl = __ballot((w >> 62) == 2);
+                const uint64_t none = __ballot((w >> 62) == 0);
+                const int stop = incl ? __ffsll((long long)incl) - 1 : 64;
+                const uint64_t need = stop == 63 || stop == 64 ? ~0ull : ((2ull << stop) - 1);
+                if (none & need) {  // a nearer tile has not published yet
+                    __builtin_amdgcn_s_sleep(2);
+                    continue;
+                }
+                uint64_t v = lane <= stop ? (w & kLbVal) : 0;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+                excl += v;
+                if (stop < 64) break;
+                top -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(status + tile, kLbIncl | (excl + agg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_excl = excl;
+            if (base + kTile >= cells) {  // last tile: the kept total
+                out_counts[0] = excl + agg;
+                out_counts[1] = cells;
+            }
+        }
+    }
+    __syncthreads();
+    uint64_t run = s_excl;
+    const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
+#pragma unroll
+    for (int r = 0; r < kFusedR; ++r) {
+        uint64_t wbase = run, tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            if (w < wid) wbase += sm[r][w];
+            tot += sm[r][w];
+        }
+        if ((m[r] >> lane) & 1ull) {
+            const size_t cell = base + (size_t)r * kBlock + threadIdx.x + g.cell0;
+            const uint32_t i = (uint32_t)(cell / g.ncx), j = (uint32_t)(cell % g.ncx);
+            const size_t k = wbase + (uint64_t)__popcll(m[r] & below);
+            // the same u, v as sample_cell (point_sampling.rs:69-70)
+            *reinterpret_cast<double2*>(uv_out + 2 * k) =
+                make_double2(((double)j + 0.5) * g.cw, ((double)i + 0.5) * g.ch);
+            xyz_out[3 * k] = X[r];
+            xyz_out[3 * k + 1] = Y[r];
+            xyz_out[3 * k + 2] = Z[r];
+        }
+        run += tot;
     }
 }
 
@@ -2090,12 +2211,19 @@ ACM_API int acm_sample_points_grid(uint32_t width, uint32_t height, size_t n_req
     return ACM_SUCCESS;
 }
 
+// two-pass: counts + offsets (2 per kSampleCells tile); single pass: one
+// status word per kFusedCells tile + the ticket
+static size_t sample_ws_words(size_t cells) {
+    const size_t nb = cells ? (cells + kSampleCells - 1) / kSampleCells : 1;
+    const size_t nt = cells ? (cells + kFusedCells - 1) / kFusedCells : 1;
+    return std::max(2 * nb, nt + 1);
+}
+
 ACM_API size_t acm_sample_points_workspace_size(const acm_camera* cam, size_t n_requested) {
     uint32_t ncx, ncy;
     if (!cam || acm_sample_points_grid(cam->width, cam->height, n_requested, &ncx, &ncy))
         return 0;
-    const size_t nb = ((size_t)ncx * ncy + kSampleCells - 1) / kSampleCells;
-    return 2 * (nb ? nb : 1) * sizeof(uint64_t);
+    return sample_ws_words((size_t)ncx * ncy) * sizeof(uint64_t);
 }
 
 ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, size_t cell_begin,
@@ -2113,18 +2241,44 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
         return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
     const size_t cells = cell_end - cell_begin;
     const size_t nb = cells ? (cells + kSampleCells - 1) / kSampleCells : 1;
-    if (workspace_bytes < 2 * nb * sizeof(uint64_t))
+    const size_t nt = cells ? (cells + kFusedCells - 1) / kFusedCells : 1;
+    if (workspace_bytes < sample_ws_words(cells) * sizeof(uint64_t))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "sample_points workspace too small");
-    if (nb > 0x7fffffffull) return fail(ACM_ERR_INVALID_ARGUMENT, "sample grid too large");
+    if (nt > 0x7fffffffull) return fail(ACM_ERR_INVALID_ARGUMENT, "sample grid too large");
     Grid g;
     g.ncx = ncx;
     g.ncy = ncy;
     g.cw = (double)cam->width / (double)ncx;  // point_sampling.rs:57
     g.ch = (double)cam->height / (double)ncy;
     g.cell0 = cell_begin;
+    hipStream_t s = (hipStream_t)stream;
+    if (g_sample_fused != 0) {
+        uint64_t* ticket = (uint64_t*)workspace;
+        uint64_t* status = ticket + 1;
+        if (hipMemsetAsync(workspace, 0, (nt + 1) * sizeof(uint64_t), s) != hipSuccess)
+            return check_launch("acm_sample_points: workspace clear");
+        if (!cells) {  // no tile runs: counts = [0 kept, 0 cells]
+            if (hipMemsetAsync(counts, 0, 2 * sizeof(uint64_t), s) != hipSuccess)
+                return check_launch("acm_sample_points: counts");
+            return ACM_SUCCESS;
+        }
+        return dispatch_model(cam->model, [&](auto tag) -> int {
+            using TagT = decltype(tag);
+            const int rr = g_sample_fused == 1   ? 4
+                           : g_sample_fused == 2 ? 8
+                           : g_sample_fused == 3 ? 16
+                                                 : SampleR<TagT>::R;
+            const size_t ntr = (cells + (size_t)kBlock * rr - 1) / ((size_t)kBlock * rr);
+            auto kern = k_sample_fused<TagT, 4>;
+            if (rr == 8) kern = k_sample_fused<TagT, 8>;
+            if (rr == 16) kern = k_sample_fused<TagT, 16>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)ntr), dim3(kBlock), 0, s, prep(*cam), g, cells,
+                               ticket, status, points_2d_out, points_3d_out, counts);
+            return check_launch("acm_sample_points");
+        });
+    }
     uint64_t* cnt = (uint64_t*)workspace;
     uint64_t* off = cnt + nb;
-    hipStream_t s = (hipStream_t)stream;
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
         hipLaunchKernelGGL((k_sample_count<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, prep(*cam),
@@ -2450,6 +2604,12 @@ ACM_API int acm_set_tuning(int key, int value) {
         if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
         const int old = g_lm_host_result;
         g_lm_host_result = value;
+        return old;
+    }
+    if (key == ACM_TUNE_SAMPLE_FUSED) {
+        if (value < -1 || value > 3) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..3");
+        const int old = g_sample_fused;
+        g_sample_fused = value;
         return old;
     }
     if (key == ACM_TUNE_FOV_UNROLL) {

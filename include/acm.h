@@ -377,6 +377,10 @@ ACM_API int acm_stream_synchronize(void *stream);
  * ACM_TUNE_LM_HOST_RESULT: acm_lm_optimize without an all-reduce callback
  * has the normal-equations kernel write its results straight into pinned
  * host memory rather than device memory plus a copy (-1 = auto = on, 0, 1).
+ * ACM_TUNE_SAMPLE_FUSED: acm_sample_points in one pass (unproject once,
+ * decoupled look-back for the output offsets; -1 = auto = per-model tile,
+ * 1 / 2 / 3 = tiles of 4 / 8 / 16 x 256 cells) or the two-pass count / scan
+ * / recompute-and-write path (0).
  * Returns the previous value or an error. */
 enum {
     ACM_TUNE_PROJECT_VARIANT = 0,
@@ -387,7 +391,8 @@ enum {
     ACM_TUNE_ALIGN_J = 5,
     ACM_TUNE_NT_LOADS = 6,
     ACM_TUNE_NT_LOADS_UNPROJECT = 7,
-    ACM_TUNE_LM_HOST_RESULT = 8
+    ACM_TUNE_LM_HOST_RESULT = 8,
+    ACM_TUNE_SAMPLE_FUSED = 9
 };
 ACM_API int acm_set_tuning(int key, int value);
 

@@ -49,7 +49,7 @@ int main() {
     acm_lm_default_config(&cfg);
     for (int key = 0; key < 10; ++key)
         for (int v = -3; v < 10; ++v) acm_set_tuning(key, v);
-    for (int key = 0; key < 9; ++key) acm_set_tuning(key, key == 2 || key == 4 ? 0 : -1);
+    for (int key = 0; key < 10; ++key) acm_set_tuning(key, key == 2 || key == 4 ? 0 : -1);
     acm_set_tuning(3, 1);
     acc += acm_normal_equations_workspace_size(2, 12345) + acm_median_workspace_size(999);
     printf("ok %d\n", std::isfinite(acc) ? 1 : 0);

@@ -276,6 +276,39 @@ def test_sample_points_vs_oracle(model, n):
         assert np.array_equal(xyz.cpu().numpy(), xyz0)
 
 
+@pytest.mark.parametrize("model", range(7))
+def test_sample_points_every_path_matches_oracle(model):
+    """The single-pass look-back kernel at every tile size (4/8/16 x 256
+    cells, ~500 tiles, a ragged last tile) and the two-pass path give the
+    oracle's kept set in the oracle's order, bit for bit, and a row-range
+    shard of the grid (odd cell offset) matches its slice of the full run."""
+    import torch
+    from apex_camera_models import _lib, util
+    from apex_camera_models.distributed import gpu_sample_points_range, grid_row_range
+    from test_oracle import SAMPLES
+    params, (w, h) = SAMPLES[model]
+    m = _model_obj(model, params, w, h)
+    n = 500_000
+    uv0, xyz0, _ = O.sample_points(model, params, w, h, n)
+    L = _lib.load()
+    ncx = int(round(np.sqrt(n * (w / h))))
+    ncy = int(round(np.sqrt(n * (h / w))))
+    try:
+        for v in (-1, 0, 1, 2, 3):
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, v)
+            uv, xyz = util.sample_points(m, n)
+            assert np.array_equal(uv.cpu().numpy(), uv0), v
+            assert rel_err(xyz.cpu().numpy(), xyz0, floor=1.0) <= TOL, v
+            if model in NO_TRANSCENDENTAL_UNPROJECT:
+                assert np.array_equal(xyz.cpu().numpy(), xyz0), v
+            fn = gpu_sample_points_range(m, n)
+            parts = [fn(*grid_row_range(ncx, ncy, r, 3)) for r in range(3)]
+            assert torch.equal(torch.cat([p[0] for p in parts]), uv), v
+            assert torch.equal(torch.cat([p[1] for p in parts]), xyz), v
+    finally:
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, -1)
+
+
 def test_full_size_kb_properties():
     """BASELINE config 2 size (10M): properties that need no oracle run over the
     whole batch, plus an oracle check of a 200k-point strided subsample."""

@@ -1,0 +1,63 @@
+"""sample_points A/B: single pass with decoupled look-back vs the two-pass
+count / scan / recompute-and-write path (ACM_TUNE_SAMPLE_FUSED), every model
+on the config-5 grid (1e8 requested cells), interleaved in one process.  The
+outputs must be bit-identical.
+
+  python tools/diag_sample.py [--cells N]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "apex-camera-models_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cells", type=int, default=100_000_000)
+    a = ap.parse_args()
+    import torch
+    from apex_camera_models import _lib, samples, util
+    from apex_camera_models.camera import MODEL_CLASSES, Resolution
+    names = ["pinhole", "rad_tan", "kannala_brandt", "double_sphere", "ucm", "eucm", "fov"]
+    L = _lib.load()
+    out = {}
+    for mid in range(7):
+        params, (w, h) = samples.SAMPLES[mid]
+        m = MODEL_CLASSES[names[mid]]._from_params([float(p) for p in params], Resolution(w, h))
+
+        def run(v):
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, v)
+            return util.sample_points(m, a.cells)
+
+        res = {v: run(v) for v in (0, 1, 2, 3)}
+        same = all(torch.equal(res[0][k], res[v][k]) for k in (0, 1) for v in (1, 2, 3))
+        kept = int(res[1][0].shape[0])
+        del res
+        cells = {}
+        for _ in range(3):
+            for v in (0, 1, 2, 3):
+                run(v)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    run(v)
+                e1.record()
+                torch.cuda.synchronize()
+                k = {0: "two_pass", 1: "fused_r4", 2: "fused_r8", 3: "fused_r16"}[v]
+                cells[k] = min(cells.get(k, 1e9), e0.elapsed_time(e1) / 3)
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, -1)
+        out[mid] = {"kept": kept, "identical": same,
+                    **{k: {"ms": round(v, 4), "Gcells_s": round(a.cells / v / 1e6, 1)}
+                       for k, v in cells.items()}}
+        print(json.dumps({"model": mid, **out[mid]}), flush=True)
+    print(json.dumps({"what": "sample_points fused vs two-pass", "cells": a.cells,
+                      "models": out}))
+
+
+if __name__ == "__main__":
+    main()
