@@ -172,9 +172,11 @@ static int g_fov_unroll = 1;
 static int g_sample_fused = -1;
 // acm_lm_optimize without an all-reduce: the normal-equations epilogue writes
 // its P*P + P + 2 results straight into pinned host memory instead of device
-// memory + a device-to-host copy (-1 = auto = on, 0 = off, 1 = on).
+// memory + a device-to-host copy.  0 = off (copy + stream synchronise), 1 =
+// pinned results + stream synchronise, 2 = pinned results + the host spins
+// on a completion word the epilogue publishes; -1 = auto = 2.
 static int g_lm_host_result = -1;
-int lm_host_result() { return g_lm_host_result != 0; }
+int lm_host_result() { return g_lm_host_result < 0 ? 2 : g_lm_host_result; }
 // Outputs above this many bytes are stored non-temporally.  Measured at 10M
 // points (profiles/r01_diag_ntl.log): project without J (170 MB out) 0.056 ms
 // nt vs 0.072 plain; a consumer that re-reads a smaller output soon after
@@ -719,9 +721,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
 // adjacent lanes read adjacent columns of one row); the R group sums of a
 // column are then added in group order by one lane.
 constexpr int kNeFinish = 1024;
+// flag != nullptr (the LM's host-polled path): after every result is out,
+// publish `seq` there with a system-scope release (out and flag are pinned
+// host memory the host spins on instead of synchronising the stream).
 template <int P>
 __global__ __launch_bounds__(kNeFinish) void k_ne_finish(const double* __restrict__ parts, int nb,
-                                                         double* __restrict__ out) {
+                                                         double* __restrict__ out,
+                                                         unsigned long long* __restrict__ flag,
+                                                         unsigned long long seq) {
     using L = NE<P>;
     constexpr int D = L::D, K = L::K;
     constexpr int R = kNeFinish / K;
@@ -754,35 +761,41 @@ __global__ __launch_bounds__(kNeFinish) void k_ne_finish(const double* __restric
         sm[t] = a;
     }
     __syncthreads();
-    if (t >= P * P + P + 2) return;
-    double v = 0.0;
-    if (t < P * P) {
-        // JtJ(i, j), i <= j: pinhole block (fx fy cx cy) and distortion block
-        const int r = t / P, c = t % P;
-        const int i = r < c ? r : c, j = r < c ? c : r;
-        if (j >= 4) {
-            const int kj = j - 4;
-            if (i == 0) v = sm[L::A_DU + kj];
-            else if (i == 1) v = sm[L::B_DV + kj];
-            else if (i == 2) v = sm[L::DU + kj];
-            else if (i == 3) v = sm[L::DV + kj];
-            else {
-                const int ki = i - 4;  // upper triangle, row-major from (ki, ki)
-                v = sm[L::DDB + ki * D - ki * (ki - 1) / 2 + (kj - ki)];
-            }
-        } else if (i == 0 && j == 0) v = sm[0];
-        else if (i == 0 && j == 2) v = sm[1];
-        else if (i == 1 && j == 1) v = sm[L::B2];
-        else if (i == 1 && j == 3) v = sm[L::B1];
-        else if (i == j) v = sm[K - 1];  // (2, 2), (3, 3): n_valid
-    } else if (t < P * P + P) {
-        v = sm[L::G + (t - P * P)];
-    } else if (t == P * P + P) {
-        v = 0.5 * sm[K - 2];
-    } else {
-        v = sm[K - 1];
+    if (t < P * P + P + 2) {
+        double v = 0.0;
+        if (t < P * P) {
+            // JtJ(i, j), i <= j: pinhole block (fx fy cx cy) and distortion block
+            const int r = t / P, c = t % P;
+            const int i = r < c ? r : c, j = r < c ? c : r;
+            if (j >= 4) {
+                const int kj = j - 4;
+                if (i == 0) v = sm[L::A_DU + kj];
+                else if (i == 1) v = sm[L::B_DV + kj];
+                else if (i == 2) v = sm[L::DU + kj];
+                else if (i == 3) v = sm[L::DV + kj];
+                else {
+                    const int ki = i - 4;  // upper triangle, row-major from (ki, ki)
+                    v = sm[L::DDB + ki * D - ki * (ki - 1) / 2 + (kj - ki)];
+                }
+            } else if (i == 0 && j == 0) v = sm[0];
+            else if (i == 0 && j == 2) v = sm[1];
+            else if (i == 1 && j == 1) v = sm[L::B2];
+            else if (i == 1 && j == 3) v = sm[L::B1];
+            else if (i == j) v = sm[K - 1];  // (2, 2), (3, 3): n_valid
+        } else if (t < P * P + P) {
+            v = sm[L::G + (t - P * P)];
+        } else if (t == P * P + P) {
+            v = 0.5 * sm[K - 2];
+        } else {
+            v = sm[K - 1];
+        }
+        out[t] = v;
     }
-    out[t] = v;
+    if (flag) {
+        __threadfence_system();
+        __syncthreads();
+        if (t == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ----------------------------------------------------- reprojection stats
@@ -2104,10 +2117,13 @@ ACM_API size_t acm_normal_equations_workspace_size(int model, size_t n) {
     return ((size_t)nq_blocks(n) + 1) * (size_t)K * sizeof(double);
 }
 
-ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* points_3d,
-                                 int layout, const double* points_2d_obs, int invalid_policy,
-                                 double* result, void* workspace, size_t workspace_bytes,
-                                 void* stream) {
+extern "C++" {
+namespace acm {
+// flag / seq: see k_ne_finish (the LM's polled path in solver.hip)
+int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_3d, int layout,
+                          const double* points_2d_obs, int invalid_policy, double* result,
+                          void* workspace, size_t workspace_bytes, void* stream,
+                          unsigned long long* flag, unsigned long long seq) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -2147,9 +2163,20 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
         };
         if (layout == ACM_LAYOUT_AOS) by_waves(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else by_waves(std::integral_constant<int, ACM_LAYOUT_SOA>{});
-        hipLaunchKernelGGL(k_ne_finish<P>, dim3(1), dim3(kNeFinish), 0, s, parts, nb, result);
+        hipLaunchKernelGGL(k_ne_finish<P>, dim3(1), dim3(kNeFinish), 0, s, parts, nb, result, flag,
+                           seq);
         return check_launch("acm_normal_equations");
     });
+}
+}  // namespace acm
+}  // extern "C++"
+
+ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* points_3d,
+                                 int layout, const double* points_2d_obs, int invalid_policy,
+                                 double* result, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+    return acm::normal_equations_impl(cam, n, points_3d, layout, points_2d_obs, invalid_policy,
+                                      result, workspace, workspace_bytes, stream, nullptr, 0);
 }
 
 ACM_API size_t acm_reprojection_stats_workspace_size(size_t n) {
@@ -2601,7 +2628,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         return old;
     }
     if (key == ACM_TUNE_LM_HOST_RESULT) {
-        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
+        if (value < -1 || value > 2) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..2");
         const int old = g_lm_host_result;
         g_lm_host_result = value;
         return old;

@@ -23,6 +23,10 @@
 namespace acm {
 int set_error(int code, const std::string& msg);  // acm.hip (one last-error slot)
 int lm_host_result();                              // acm.hip, ACM_TUNE_LM_HOST_RESULT
+int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_3d, int layout,
+                          const double* points_2d_obs, int invalid_policy, double* result,
+                          void* workspace, size_t workspace_bytes, void* stream,
+                          unsigned long long* flag, unsigned long long seq);
 }
 
 namespace {
@@ -331,10 +335,15 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
     std::vector<double> h(R);
     // Without an all-reduce the epilogue kernel writes the R results straight
     // into pinned, device-mapped host memory: no device-to-host copy launch
-    // per evaluation (one buffer per host thread, kept for the process).
+    // per evaluation (one buffer per host thread, kept for the process).  In
+    // mode 2 it also publishes a sequence number in the buffer's last word,
+    // and the host spins on that word instead of synchronising the stream.
     static thread_local double* pinned = nullptr;
+    static thread_local unsigned long long seq = 0;
+    const int host_mode = allreduce ? 0 : acm::lm_host_result();
     double* res_out = d_res;
-    if (!allreduce && acm::lm_host_result()) {
+    unsigned long long* flag = nullptr;
+    if (host_mode) {
         if (!pinned) {
             void* p = nullptr;
             if (hipHostMalloc(&p, 128 * sizeof(double),
@@ -344,7 +353,10 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
             else
                 (void)hipGetLastError();
         }
-        if (pinned) res_out = pinned;
+        if (pinned) {
+            res_out = pinned;
+            if (host_mode == 2) flag = reinterpret_cast<unsigned long long*>(pinned + 127);
+        }
     }
     acm_lm_summary sum;
     std::memset(&sum, 0, sizeof(sum));
@@ -357,14 +369,32 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
     auto eval = [&](const double* x, double* A, double* g, double* F, double* nv) -> int {
         acm_camera c = *cam;
         for (int i = 0; i < P; ++i) c.params[i] = x[i];
-        int rc = acm_normal_equations(&c, n, points_3d, layout, points_2d, cfg->invalid_policy,
-                                      res_out, workspace, ne_ws, stream);
+        const unsigned long long want = flag ? ++seq : 0;
+        int rc = acm::normal_equations_impl(&c, n, points_3d, layout, points_2d,
+                                            cfg->invalid_policy, res_out, workspace, ne_ws, stream,
+                                            flag, want);
         if (rc) return rc;
         if (allreduce) {
             rc = allreduce(allreduce_ctx, d_res, (size_t)R, stream);
             if (rc) return sfail(ACM_ERR_HIP, "all-reduce callback failed");
         }
-        if (res_out != d_res) {
+        if (flag) {
+            // spin on the completion word; every 256 polls ask the stream, so
+            // a failed launch surfaces as an error instead of a hang
+            for (unsigned spin = 1;; ++spin) {
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == want) break;
+                if ((spin & 255) == 0) {
+                    const hipError_t q = hipStreamQuery(s);
+                    if (q == hipSuccess) {
+                        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == want) break;
+                        return sfail(ACM_ERR_HIP, "LM: completion word not published");
+                    }
+                    if (q != hipErrorNotReady) return sfail(ACM_ERR_HIP, "LM: stream failed");
+                }
+                __builtin_ia32_pause();
+            }
+            std::memcpy(h.data(), res_out, R * sizeof(double));
+        } else if (res_out != d_res) {
             if (hip_ok(hipStreamSynchronize(s))) return sfail(ACM_ERR_HIP, "LM: stream failed");
             std::memcpy(h.data(), res_out, R * sizeof(double));
         } else if (hip_ok(hipMemcpyAsync(h.data(), d_res, R * sizeof(double),

@@ -376,7 +376,9 @@ ACM_API int acm_stream_synchronize(void *stream);
  * for acm_unproject's pixel stream (-1 = auto = off, 0, 1).
  * ACM_TUNE_LM_HOST_RESULT: acm_lm_optimize without an all-reduce callback
  * has the normal-equations kernel write its results straight into pinned
- * host memory rather than device memory plus a copy (-1 = auto = on, 0, 1).
+ * host memory rather than device memory plus a copy: 0 = off, 1 = on with a
+ * stream synchronisation, 2 = on with the host spinning on a completion
+ * word the kernel publishes; -1 = auto = 2.
  * ACM_TUNE_SAMPLE_FUSED: acm_sample_points in one pass (unproject once,
  * decoupled look-back for the output offsets; -1 = auto = per-model tile,
  * 1 / 2 / 3 = tiles of 4 / 8 / 16 x 256 cells) or the two-pass count / scan

@@ -1,6 +1,8 @@
 """LM loop overhead on config-3 data (KB-sampled correspondences, DS target):
 wall time of acm_lm_optimize vs evaluations x the normal-equation kernel
-time, i.e. the host / launch / copy cost per evaluation.
+time, i.e. the host / launch / copy cost per evaluation, for each
+ACM_TUNE_LM_HOST_RESULT mode (0 copy + sync, 1 pinned + sync, 2 pinned +
+spin on the completion word; the reported wall is mode 2, the default).
 
   python tools/diag_lm.py [--points N]
 """
@@ -43,18 +45,26 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ne_ms = e0.elapsed_time(e1) / 20
-    walls, res = [], None
-    for _ in range(4):
-        m = conversion._init_target("double_sphere", src)
-        m._set_params(list(p0))
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        res = LevenbergMarquardt(LevenbergMarquardtConfig()).optimize(
-            m, xyz, uv, bounds=CONVERTER_BOUNDS["double_sphere"])
-        torch.cuda.synchronize()
-        walls.append((time.perf_counter() - t0) * 1e3)
-    wall = min(walls[1:])
+    from apex_camera_models import _lib
+    L = _lib.load()
+    by_mode = {}
+    res = None
+    for _ in range(3):
+        for mode in (0, 1, 2):  # ACM_TUNE_LM_HOST_RESULT: copy / pinned + sync / pinned + spin
+            L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, mode)
+            m = conversion._init_target("double_sphere", src)
+            m._set_params(list(p0))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = LevenbergMarquardt(LevenbergMarquardtConfig()).optimize(
+                m, xyz, uv, bounds=CONVERTER_BOUNDS["double_sphere"])
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3
+            by_mode[mode] = min(by_mode.get(mode, 1e9), ms)
+    L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, -1)
+    wall = by_mode[2]
     print(json.dumps({"what": "LM loop overhead", "points": n, "lm_wall_ms": round(wall, 3),
+                      "lm_wall_ms_by_host_result_mode": {k: round(v, 3) for k, v in by_mode.items()},
                       "evaluations": res.evaluations, "iterations": res.iterations,
                       "ne_ms": round(ne_ms, 4),
                       "overhead_per_eval_ms": round((wall - res.evaluations * ne_ms)
