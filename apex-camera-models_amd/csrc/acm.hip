@@ -514,14 +514,16 @@ struct NE {
 };
 
 // Per-model (waves, points per lane step) of k_normal_eq: the fastest cell of
-// the interleaved {1,3,4} x {1,2} x nt-loads sweep (tools/bench_configs.py
-// --configs 3ne, profiles/r01_ne_sweep.log, 10M points).  All cells give the
-// same sums up to summation order.
+// the interleaved {1,3,4} x {1, 2, 3 = one point two steps ahead} sweep with
+// nt loads (tools/bench_configs.py --configs 3ne, profiles/r01s7_ne_sweep.log,
+// 10M points).  All cells give the same sums up to summation order.
 template <class TagT> struct NeDefault { static constexpr int W = 3, U = 1; };
 template <> struct NeDefault<Tag<RadTan>> { static constexpr int W = 3, U = 2; };
+template <> struct NeDefault<Tag<KannalaBrandt>> { static constexpr int W = 1, U = 3; };
+template <> struct NeDefault<Tag<DoubleSphere>> { static constexpr int W = 1, U = 3; };
 template <> struct NeDefault<Tag<Ucm>> { static constexpr int W = 3, U = 2; };
-template <> struct NeDefault<Tag<Eucm>> { static constexpr int W = 3, U = 2; };
-template <> struct NeDefault<Tag<Fov>> { static constexpr int W = 4, U = 1; };
+template <> struct NeDefault<Tag<Eucm>> { static constexpr int W = 3, U = 3; };
+template <> struct NeDefault<Tag<Fov>> { static constexpr int W = 3, U = 3; };
 
 constexpr int kNeMaxBlocks = 2048;  // reprojection stats / median partials
 constexpr int kNqMaxBlocks = 2048;  // normal equations: 8 workgroups per CU
@@ -651,7 +653,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             acc[K - 2] += sent2;
         }
     };
-    if constexpr (U == 1) {
+    if constexpr (U == 3) {
+        // one point per lane step, loads issued two steps ahead (twice the
+        // bytes in flight of U = 1 for 5 more registers of data)
+        double x0 = 0, y0 = 0, z0 = 1, x1 = 0, y1 = 0, z1 = 1;
+        double2 o0 = make_double2(0.0, 0.0), o1 = make_double2(0.0, 0.0);
+        if (i < n) {
+            load_point<LAYOUT, NTL>(pts, n, i, x0, y0, z0);
+            o0 = ld2<NTL>(obs + 2 * i);
+        }
+        if (i + stride < n) {
+            load_point<LAYOUT, NTL>(pts, n, i + stride, x1, y1, z1);
+            o1 = ld2<NTL>(obs + 2 * (i + stride));
+        }
+        for (; i < n; i += stride) {
+            const size_t i2 = i + 2 * stride;
+            double x2 = 0, y2 = 0, z2 = 1;
+            double2 o2 = make_double2(0.0, 0.0);
+            if (i2 < n) {
+                load_point<LAYOUT, NTL>(pts, n, i2, x2, y2, z2);
+                o2 = ld2<NTL>(obs + 2 * i2);
+            }
+            accumulate(x0, y0, z0, o0);
+            x0 = x1; y0 = y1; z0 = z1; o0 = o1;
+            x1 = x2; y1 = y2; z1 = z2; o1 = o2;
+        }
+    } else if constexpr (U == 1) {
         double x = 0, y = 0, z = 1;
         double2 o = make_double2(0.0, 0.0);
         if (kPrefetch && i < n) {
@@ -2149,6 +2176,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
             const bool ntl = g_nt_loads != 0;
             auto kern = ntl ? k_normal_eq<TagT, LAY, W, 1, true> : k_normal_eq<TagT, LAY, W, 1, false>;
             if (un == 2) kern = ntl ? k_normal_eq<TagT, LAY, W, 2, true> : k_normal_eq<TagT, LAY, W, 2, false>;
+            if (un == 3) kern = ntl ? k_normal_eq<TagT, LAY, W, 3, true> : k_normal_eq<TagT, LAY, W, 3, false>;
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
@@ -2603,8 +2631,8 @@ ACM_API int acm_set_tuning(int key, int value) {
         return old;
     }
     if (key == ACM_TUNE_NE_UNROLL) {
-        if (value != 0 && value != 1 && value != 2)
-            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 0 (per-model default), 1 or 2");
+        if (value < 0 || value > 3)
+            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 0 (per-model default), 1, 2 or 3");
         const int old = g_ne_unroll;
         g_ne_unroll = value;
         return old;

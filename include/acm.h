@@ -366,7 +366,8 @@ ACM_API int acm_stream_synchronize(void *stream);
  * minimum waves per SIMD the normal-equations kernel is compiled for
  * (0 = per-model default, 1, 3, 4).  ACM_TUNE_FOV_UNROLL: points per lane step of the FOV
  * grid search (1 = default, 2, 4).  ACM_TUNE_NE_UNROLL: points per lane step
- * of the normal-equations kernel (0 = per-model default, 1, 2).
+ * of the normal-equations kernel (0 = per-model default, 1, 2; 3 = one point
+ * per step with its loads issued two steps ahead).
  * ACM_TUNE_ALIGN_J: kernel of +Jacobian launches of acm_project /
  * acm_residual_jacobian: -1 = auto (default) = line-aligned store windows
  * through LDS, 0 = one point per lane with direct stores, 1 = aligned.

@@ -184,7 +184,7 @@ def test_normal_equations_every_tuning_cell(model):
     L = _lib.load()
     try:
         for wv in (0, 1, 3, 4):
-            for un in (0, 1, 2):
+            for un in (0, 1, 2, 3):
                 for ntl in (-1, 0):
                     L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)
                     L.acm_set_tuning(_lib.TUNE_NE_UNROLL, un)

@@ -135,8 +135,9 @@ def config3_ne_all(n):
         out = torch.empty((P * P + P + 2,), dtype=torch.float64, device="cuda")
         L = _lib.load()
         res = {}
-        combos = [(0, 0, -1)] + [(wv, un, nl) for wv in (1, 3, 4) for un in (1, 2)
-                                 for nl in (0, 1)]
+        # nt loads measured 5-11% faster in every cell (profiles/r01_ne_sweep.log);
+        # unroll 3 = one point per step, loads two steps ahead
+        combos = [(0, 0, -1)] + [(wv, un, 1) for wv in (1, 3, 4) for un in (1, 2, 3)]
         for rep in range(2):  # interleaved A/B: register target x lane step x nt loads
             for wv, un, nl in combos:
                 L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)
