@@ -15,6 +15,11 @@
 // Status decisions are computed branch-free where possible so a wave does
 // not diverge on the rare failing point; the caller selects outputs.
 //
+// KB's projection (double) takes r, 1/r and its atan2 quotient from the
+// hardware rsq / rcp estimates + Newton steps (~1 ulp; ACM_IEEE_MATH builds
+// the IEEE sqrt / divisions instead): like its polynomial atan2 it is held
+// to 1e-10 against the reference, with the status decisions exact.
+//
 // project<WJ, FAST>: FAST = true (used only by the fused normal-equations
 // kernel, whose sums are held to 1e-10 anyway and are summed in a different
 // order than the reference) replaces the divisions by a per-point denominator
@@ -95,6 +100,31 @@ __device__ __forceinline__ double atan2_ge0(double y, double x) {
     return atan2(y, x);
 }
 __device__ __forceinline__ float atan2_ge0(float y, float x) { return atan2(y, x); }
+
+// 1/sqrt(a) and 1/a from the hardware estimates (v_rsq_f64 / v_rcp_f64)
+// with two Newton-Raphson steps each: within ~1 ulp for a in
+// [2^-1000, 2^1000] (callers check the range and take the IEEE forms
+// outside it).  Used only where the model already differs from the
+// reference in the last bits (KB's atan2 is a polynomial) and no status
+// decision depends on the value.
+__device__ __forceinline__ double rsq_nr(double a) {
+    double y = __builtin_amdgcn_rsq(a);
+    const double h = 0.5 * a;
+    double e = fma(-h * y, y, 0.5);
+    y = fma(y, e, y);
+    e = fma(-h * y, y, 0.5);
+    return fma(y, e, y);
+}
+__device__ __forceinline__ double rcp_nr(double a) {
+    double y = __builtin_amdgcn_rcp(a);
+    double e = fma(-a, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-a, y, 1.0);
+    return fma(y, e, y);
+}
+__device__ __forceinline__ bool nr_range(double a) {
+    return a >= 0x1p-1000 && a <= 0x1p1000;
+}
 
 // sin and cos of theta in [0, 2] (KB's unprojection angle, at most ~pi/2):
 // theta * S(theta^2) and C(theta^2), S and C the degree-10 Chebyshev
@@ -339,18 +369,50 @@ struct KannalaBrandt {
         const T k1 = c.p[4], k2 = c.p[5], k3 = c.p[6], k4 = c.p[7];
         uint8_t st = z < T(0) ? ST_POINT_IS_OUT_SIDE_IMAGE
                               : (z < T(kEps) ? ST_POINT_AT_CAMERA_CENTER : ST_OK);
-        T r = sqrt(x * x + y * y);  // :363-364
-        T theta = atan2_ge0(r, z);  // :365 (r >= 0)
+        const T r2 = x * x + y * y;  // :363-364
+        T r, theta, ir = T(0);
+        bool axis;
+#ifndef ACM_IEEE_MATH
+        if constexpr (sizeof(T) == 8) {
+            // r, 1/r and the atan2 quotient from rsq / rcp + Newton (~1 ulp;
+            // the model is already held to 1e-10, not bit-exactness).  The
+            // axis test r < EPS (:375) stays exact: only r2 < 1e-30 can pass
+            // it, and that rare case takes the IEEE sqrt.
+            if (nr_range(r2) && nr_range(z) && z < T(INFINITY)) {
+                ir = rsq_nr(r2);
+                r = r2 * ir;
+                const bool swap = r > z;  // atan2(r, z), z > 0 finite
+                const T q = swap ? z * ir : r * rcp_nr(z);
+                const T at = atan01(q);
+                theta = swap ? T(1.5707963267948966) - at : at;
+            } else {
+                r = sqrt(r2);
+                theta = atan2_ge0(r, z);  // :365 (r >= 0)
+                ir = T(1) / r;
+            }
+            axis = false;
+            if (r2 < T(1e-30)) axis = sqrt(r2) < T(kEps);
+        } else
+#endif
+        {
+            r = sqrt(r2);
+            theta = atan2_ge0(r, z);  // :365 (r >= 0)
+            axis = r < T(kEps);  // :375
+            if (FAST) ir = T(1) / r;
+        }
         T theta2 = theta * theta;
         T theta3 = theta2 * theta;
         T theta5 = theta3 * theta2;
         T theta7 = theta5 * theta2;
         T theta9 = theta7 * theta2;
         T theta_d = theta + k1 * theta3 + k2 * theta5 + k3 * theta7 + k4 * theta9;
-        const bool axis = r < T(kEps);  // :375
-        const T ir = FAST ? T(1) / r : T(0);
-        T x_r = axis ? T(0) : (FAST ? x * ir : x / r);
-        T y_r = axis ? T(0) : (FAST ? y * ir : y / r);
+#ifndef ACM_IEEE_MATH
+        constexpr bool kMul = FAST || sizeof(T) == 8;
+#else
+        constexpr bool kMul = FAST;
+#endif
+        T x_r = axis ? T(0) : (kMul ? x * ir : x / r);
+        T y_r = axis ? T(0) : (kMul ? y * ir : y / r);
         u = fx * theta_d * x_r + cx;  // :390
         v = fy * theta_d * y_r + cy;
         if (WJ) {
