@@ -70,6 +70,29 @@ static int dispatch_model(int model, F&& f) {
     }
 }
 
+// Uniform subexpressions of the unprojections, in the reference's operation
+// order (IEEE results: the host and a lane compute the same bits).
+template <class T>
+__host__ __device__ inline void unproject_consts(int model, const T* p, T* uk) {
+    uk[0] = uk[1] = T(0);
+    if (model == ACM_DOUBLE_SPHERE) {
+        uk[0] = T(1) / (T(2) * p[4] - T(1));  // double_sphere.rs:205
+    } else if (model == ACM_UCM) {
+        const T gamma = T(1) - p[4];
+        uk[0] = p[4] / gamma;                          // xi, ucm.rs:343
+        uk[1] = gamma * gamma / (T(2) * p[4] - T(1));  // ucm.rs:180
+    } else if (model == ACM_EUCM) {
+        uk[0] = T(1) / p[5] * (T(2) * p[4] - T(1));  // eucm.rs:196 (precedence quirk)
+    }
+}
+
+// The unprojection kernels' camera argument: acm_camera plus the host-side
+// constants of Cam (prep): RN(1 / fx), RN(1 / fy) and unproject_consts.
+struct CamArg : acm_camera {
+    double ifx, ify;
+    double uk[2];
+};
+
 template <class T>
 __device__ __forceinline__ Cam<T> make_cam(const acm_camera& c) {
     Cam<T> k;
@@ -79,6 +102,25 @@ __device__ __forceinline__ Cam<T> make_cam(const acm_camera& c) {
     k.h = (T)(double)c.height;
     k.wi = c.width;
     k.hi = c.height;
+    k.ifx = k.ify = T(0);  // divide
+    unproject_consts<T>(c.model, k.p, k.uk);
+    return k;
+}
+
+template <class T>
+__device__ __forceinline__ Cam<T> make_cam(const CamArg& c) {
+    static_assert(sizeof(T) == 8, "the unprojection kernels run in double");
+    Cam<T> k;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) k.p[i] = c.params[i];
+    k.w = (double)c.width;
+    k.h = (double)c.height;
+    k.wi = c.width;
+    k.hi = c.height;
+    k.ifx = c.ifx;
+    k.ify = c.ify;
+    k.uk[0] = c.uk[0];
+    k.uk[1] = c.uk[1];
     return k;
 }
 
@@ -170,6 +212,10 @@ static int g_fov_unroll = 1;
 // per-model tile (SampleR), 0 = the two-pass count / scan / write path,
 // 1 / 2 / 3 = single pass with tiles of 4 / 8 / 16 x 256 cells.
 static int g_sample_fused = -1;
+// Unprojections: (u - cx) / fx and (v - cy) / fy from the host's RN(1 / fx),
+// RN(1 / fy) (div_by_f, bit-identical) instead of two IEEE divisions per
+// point: -1 = auto = on, 0 = off, 1 = on.
+static int g_unproject_rcp = -1;
 // acm_lm_optimize without an all-reduce: the normal-equations epilogue writes
 // its P*P + P + 2 results straight into pinned host memory instead of device
 // memory + a device-to-host copy.  0 = off (copy + stream synchronise), 1 =
@@ -408,7 +454,7 @@ __device__ __forceinline__ void st1d(double* p, double v) {
 }
 
 template <class TagT, int LAYOUT, bool NT, bool NTL>
-__global__ __launch_bounds__(kBlock) void k_unproject(acm_camera cam, size_t n,
+__global__ __launch_bounds__(kBlock) void k_unproject(CamArg cam, size_t n,
                                                       const double* __restrict__ uv,
                                                       double* __restrict__ rays,
                                                       uint8_t* __restrict__ status) {
@@ -1012,7 +1058,7 @@ constexpr int kSampleR = 16;
 constexpr size_t kSampleCells = (size_t)kBlock * kSampleR;
 
 template <class TagT>
-__global__ __launch_bounds__(kBlock) void k_sample_count(acm_camera cam, Grid g, size_t cells,
+__global__ __launch_bounds__(kBlock) void k_sample_count(CamArg cam, Grid g, size_t cells,
                                                          uint64_t* __restrict__ counts) {
     const Cam<double> c = make_cam<double>(cam);
     const size_t base = (size_t)blockIdx.x * kSampleCells;
@@ -1072,7 +1118,7 @@ __global__ __launch_bounds__(1024) void k_scan_counts(const uint64_t* __restrict
 }
 
 template <class TagT>
-__global__ __launch_bounds__(kBlock) void k_sample_write(acm_camera cam, Grid g, size_t cells,
+__global__ __launch_bounds__(kBlock) void k_sample_write(CamArg cam, Grid g, size_t cells,
                                                          const uint64_t* __restrict__ offsets,
                                                          double* __restrict__ uv_out,
                                                          double* __restrict__ xyz_out) {
@@ -1129,7 +1175,7 @@ constexpr size_t kFusedCells = (size_t)kBlock * kFusedRMin;
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
 
 template <class TagT, int kFusedR>
-__global__ __launch_bounds__(kBlock) void k_sample_fused(acm_camera cam, Grid g, size_t cells,
+__global__ __launch_bounds__(kBlock) void k_sample_fused(CamArg cam, Grid g, size_t cells,
                                                          uint64_t* __restrict__ ticket,
                                                          uint64_t* __restrict__ status,
                                                          double* __restrict__ uv_out,
@@ -1883,9 +1929,21 @@ static unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 // launch.  FOV: params[8] = tan(w / 2) (fov.rs:297, :340), evaluated once by
 // the host libm (the same glibc tan the reference's f64::tan calls) instead
 // of once per lane by OCML.
-static acm_camera prep(acm_camera c) {
+// Unprojection launches also carry RN(1 / fx), RN(1 / fy) (0 outside the
+// range div_by_f is exact in) and the model's uniform subexpressions.
+static CamArg prep(acm_camera c) {
     if (c.model == ACM_FOV) c.params[8] = std::tan(c.params[4] / 2.0);
-    return c;
+    CamArg a;
+    static_cast<acm_camera&>(a) = c;
+    auto recip = [](double f) {
+        const double af = std::fabs(f);
+        return af >= 0x1p-500 && af <= 0x1p500 ? 1.0 / f : 0.0;
+    };
+    const bool rcp = g_unproject_rcp != 0;
+    a.ifx = rcp ? recip(c.params[0]) : 0.0;
+    a.ify = rcp ? recip(c.params[1]) : 0.0;
+    unproject_consts<double>(c.model, c.params, a.uk);
+    return a;
 }
 
 static int check_cam(const acm_camera* cam) {
@@ -2659,6 +2717,12 @@ ACM_API int acm_set_tuning(int key, int value) {
         if (value < -1 || value > 2) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..2");
         const int old = g_lm_host_result;
         g_lm_host_result = value;
+        return old;
+    }
+    if (key == ACM_TUNE_UNPROJECT_RCP) {
+        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
+        const int old = g_unproject_rcp;
+        g_unproject_rcp = value;
         return old;
     }
     if (key == ACM_TUNE_SAMPLE_FUSED) {

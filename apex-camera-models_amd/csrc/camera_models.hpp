@@ -216,7 +216,25 @@ struct Cam {
     T p[9];
     T w, h;        // resolution as f64, like `width as f64` in the reference
     uint32_t wi, hi;
+    // Per-camera constants of the unprojections (acm.hip make_cam / prep):
+    // ifx, ify = RN(1 / fx), RN(1 / fy) from the host for div_by_f (0 = divide
+    // instead), and uk = uniform subexpressions the reference evaluates per
+    // point (IEEE results, identical wherever they are computed).
+    T ifx, ify;
+    T uk[2];
 };
+
+// (u - cx) / fx with fx uniform: RN(a / b) from the host's RN(1 / b) and the
+// Markstein correction of div_rn, bit-identical to the IEEE division (see
+// div_shared) while |a| and |b| lie in [2^-500, 2^500]; anything else (and
+// every float) divides.  Saves an IEEE division sequence per coordinate.
+template <class T>
+__device__ __forceinline__ T div_by_f(T a, T b, T ib) {
+    if constexpr (sizeof(T) == 8) {
+        if (ib != T(0) && div_safe(a)) return div_rn(a, ib, b);
+    }
+    return a / b;
+}
 
 // ---------------------------------------------------------------- Pinhole
 template <class T>
@@ -244,8 +262,8 @@ struct Pinhole {
                                                         T& Z) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
         const bool out = u < T(0) || u >= c.w || v < T(0) || v >= c.h;
-        T mx = (u - cx) / fx;
-        T my = (v - cy) / fy;
+        T mx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
+        T my = div_by_f(v - cy, fy, c.ify);
         T r2 = mx * mx + my * my;
         T norm = sqrt(T(1) + r2);
         T ninv = T(1) / norm;
@@ -305,8 +323,8 @@ struct RadTan {
             X = Y = Z = T(NAN);
             return ST_POINT_IS_OUT_SIDE_IMAGE;
         }
-        const T tx = (u - cx) / fx;
-        const T ty = (v - cy) / fy;
+        const T tx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
+        const T ty = div_by_f(v - cy, fy, c.ify);
         T px = tx, py = ty;
         uint8_t st = ST_OK;
         for (unsigned it = 0; it < 100u; ++it) {
@@ -433,8 +451,8 @@ struct KannalaBrandt {
             X = Y = Z = T(NAN);
             return ST_POINT_IS_OUT_SIDE_IMAGE;  // :447-455
         }
-        T mx = (u - cx) / fx;
-        T my = (v - cy) / fy;
+        T mx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
+        T my = div_by_f(v - cy, fy, c.ify);
         T ru = sqrt(mx * mx + my * my);
         ru = fmin(ru, T(kPi / 2.0));  // :467, f64::min semantics
         T theta = ru;
@@ -519,10 +537,11 @@ struct DoubleSphere {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
         const T alpha = c.p[4], xi = c.p[5];
         T gamma_ds = T(1) - alpha;
-        T mx = (u - cx) / fx;
-        T my = (v - cy) / fy;
+        T mx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
+        T my = div_by_f(v - cy, fy, c.ify);
         T r_squared = (mx * mx) + (my * my);
-        const bool cond = !(alpha > T(0.5) && r_squared > T(1) / (T(2) * alpha - T(1)));
+        // c.uk[0] = 1 / (2 alpha - 1)
+        const bool cond = !(alpha > T(0.5) && r_squared > c.uk[0]);
         const bool reject = alpha != T(0) && !cond;
         T mz = (T(1) - alpha * alpha * r_squared) /
                (alpha * sqrt(T(1) - (T(2) * alpha - T(1)) * r_squared) + gamma_ds);
@@ -572,14 +591,14 @@ struct Ucm {
                                                         T& Z) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], alpha = c.p[4];
         T gamma = T(1) - alpha;
-        T xi = alpha / gamma;
-        T mx = (u - cx) / fx * gamma;
-        T my = (v - cy) / fy * gamma;
+        T xi = c.uk[0];  // alpha / gamma
+        T mx = div_by_f(u - cx, fx, c.ifx) * gamma;  // (u - cx) / fx * gamma
+        T my = div_by_f(v - cy, fy, c.ify) * gamma;
         T r_squared = mx * mx + my * my;
         T num = xi + sqrt(T(1) + (T(1) - xi * xi) * r_squared);
         T denom = T(1) - r_squared;
-        const bool cond = alpha > T(0.5) ? (r_squared <= gamma * gamma / (T(2) * alpha - T(1)))
-                                         : true;
+        // c.uk[1] = gamma * gamma / (2 alpha - 1)
+        const bool cond = alpha > T(0.5) ? (r_squared <= c.uk[1]) : true;
         T coeff = num / denom;
         T px = coeff * mx, py = coeff * my, pz = coeff - xi;
         T n = sqrt(px * px + py * py + pz * pz);
@@ -632,14 +651,15 @@ struct Eucm {
                                                         T& Z) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
         const T alpha = c.p[4], beta = c.p[5];
-        T mx = (u - cx) / fx;
-        T my = (v - cy) / fy;
+        T mx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
+        T my = div_by_f(v - cy, fy, c.ify);
         T r_squared = mx * mx + my * my;
         T gamma = T(1) - alpha;
         T num = T(1) - r_squared * alpha * alpha * beta;
         T det = T(1) - (alpha - gamma) * beta * r_squared;
         T denom = gamma + alpha * sqrt(det);
-        const bool cond = !(alpha > T(0.5) && r_squared > (T(1) / beta * (T(2) * alpha - T(1))));
+        // c.uk[0] = 1 / beta * (2 alpha - 1)
+        const bool cond = !(alpha > T(0.5) && r_squared > c.uk[0]);
         T mz = num / denom;
         T n = sqrt(mx * mx + my * my + mz * mz);
         const T nq[3] = {mx, my, mz};
@@ -692,8 +712,8 @@ struct Fov {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], wf = c.p[4];
         const T tan_w_2 = c.p[8];  // tan(w / 2), host-precomputed
         T mul2 = tan_w_2 * T(2);
-        T mx = (u - cx) / fx;
-        T my = (v - cy) / fy;
+        T mx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
+        T my = div_by_f(v - cy, fy, c.ify);
         T rd = sqrt(mx * mx + my * my);
         T px = mx, py = my;
         if (mul2 > T(kEpsSqrt) && rd > T(kEpsSqrt)) {

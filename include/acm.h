@@ -384,6 +384,10 @@ ACM_API int acm_stream_synchronize(void *stream);
  * decoupled look-back for the output offsets; -1 = auto = per-model tile,
  * 1 / 2 / 3 = tiles of 4 / 8 / 16 x 256 cells) or the two-pass count / scan
  * / recompute-and-write path (0).
+ * ACM_TUNE_UNPROJECT_RCP: unprojections (acm_unproject, acm_sample_points*)
+ * divide by fx, fy through the host's correctly rounded 1/fx, 1/fy and one
+ * FMA correction, bit-identical to the division (-1 = auto = on, 0 = plain
+ * IEEE divisions, 1 = on).
  * Returns the previous value or an error. */
 enum {
     ACM_TUNE_PROJECT_VARIANT = 0,
@@ -395,7 +399,8 @@ enum {
     ACM_TUNE_NT_LOADS = 6,
     ACM_TUNE_NT_LOADS_UNPROJECT = 7,
     ACM_TUNE_LM_HOST_RESULT = 8,
-    ACM_TUNE_SAMPLE_FUSED = 9
+    ACM_TUNE_SAMPLE_FUSED = 9,
+    ACM_TUNE_UNPROJECT_RCP = 10
 };
 ACM_API int acm_set_tuning(int key, int value);
 
