@@ -478,13 +478,31 @@ struct KannalaBrandt {
             else { theta = T(0); }
         }
         const bool small = fabs(ru) < T(kEps);
+        T s, co;
+        sincos_0_2(theta, &s, &co);  // polynomial on [0, 2], OCML sincos beyond
+#ifndef ACM_IEEE_MATH
+        if constexpr (sizeof(T) == 8) {
+            // Everything after the Newton loop only shapes the ray: no status
+            // decision depends on it, and the ray is held to 1e-10 anyway
+            // (sin / cos are polynomials).  1 / ru and 1 / |p| from rcp / rsq
+            // + Newton (~1 ulp) instead of two IEEE divisions and a sqrt.
+            const T ir = nr_range(ru) ? rcp_nr(ru) : T(1) / ru;
+            const T xc = small ? T(0) : mx * ir;  // mx / ru
+            const T yc = small ? T(0) : my * ir;
+            const T px = s * xc, py = s * yc;
+            const T n2 = px * px + py * py + co * co;
+            const T in = nr_range(n2) ? rsq_nr(n2) : T(1) / sqrt(n2);
+            X = px * in;
+            Y = py * in;
+            Z = co * in;
+            return converged ? ST_OK : ST_NUMERICAL_ERROR;
+        }
+#endif
         const T mxy[2] = {mx, my};
         T c2[2];
         div_shared(mxy, ru, c2);  // mx / ru, my / ru
         T xc = small ? T(0) : c2[0];
         T yc = small ? T(0) : c2[1];
-        T s, co;
-        sincos_0_2(theta, &s, &co);  // polynomial on [0, 2], OCML sincos beyond
         T px = s * xc, py = s * yc;
         T n = sqrt(px * px + py * py + co * co);
         const T nq[3] = {px, py, co};

@@ -207,21 +207,25 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(a.steps)]
+    # One HIP event pair on the launch stream around the K back-to-back
+    # launches: the average launch duration includes the (sub-microsecond)
+    # gaps between launches, so `achieved` is conservative.  An event pair
+    # around every launch put ~5 us of extra gap between launches (wall
+    # 0.2499 vs 0.2433 ms per step, profiles/r01s8_diag_bench_gaps.log).
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for e0, e1 in ev:
-        e0.record(stream)
+    e0.record(stream)
+    for _ in range(a.steps):
         step()
-        e1.record(stream)
+    e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / a.steps
+    kern_ms = e0.elapsed_time(e1) / a.steps
 
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
                      device=dev if backend == "nccl" else "cpu")

@@ -1,8 +1,11 @@
-"""KB projection A/B in one process: the default library (r, 1/r and
+"""KB projection / unprojection A/B in one process: the default library (r, 1/r and
 the atan2 quotient from v_rsq / v_rcp + Newton) against a build with the
 IEEE sqrt / divisions (-DACM_IEEE_MATH: `make -C apex-camera-models_amd ieee`
 builds lib/libacm_ieee.so).  Project with and without the Jacobian, 10M points; also the
-largest relative difference between the two builds' outputs.
+largest relative difference between the two builds' outputs.  Then KB
+unproject (10M pixels, the projections of the bench cloud): the default
+library takes 1 / ru and 1 / |p| after the Newton loop from v_rcp / v_rsq +
+Newton; the IEEE build divides.
 
   python tools/diag_fast_math.py
 """
@@ -29,6 +32,8 @@ def main():
                                       ctypes.c_uint32, ctypes.c_uint32]
         L.acm_project.argtypes = [ctypes.POINTER(_lib.AcmCamera), ctypes.c_size_t, vp,
                                   ctypes.c_int, vp, vp, vp, vp]
+        L.acm_unproject.argtypes = [ctypes.POINTER(_lib.AcmCamera), ctypes.c_size_t, vp, vp,
+                                    ctypes.c_int, vp, vp]
     n = 10_000_000
     pts = samples.synthetic_points_device(n)
     sh = torch.cuda.current_stream().cuda_stream
@@ -83,6 +88,32 @@ def main():
                           "points": n, "ms": {k: round(v, 4) for k, v in cells.items()},
                           "status_identical": bool(torch.equal(a_st, b_st)),
                           "max_rel_uv_diff": rel_uv, "max_rel_jac_diff": rel_j}), flush=True)
+
+        # unprojection of the projected cloud
+        uvin = torch.nan_to_num(outs["nr"][0], nan=1.0).contiguous()
+        un = {k: (torch.empty((n, 3), dtype=torch.float64, device="cuda"),
+                  torch.empty((n,), dtype=torch.uint8, device="cuda")) for k in libs}
+
+        def ucall(k):
+            rays, st = un[k]
+            return libs[k].acm_unproject(ctypes.byref(cams[k]), n, uvin.data_ptr(),
+                                         rays.data_ptr(), 0, st.data_ptr(), sh)
+
+        ucells = {}
+        for _ in range(8):
+            for k in libs:
+                ucells[k] = min(ucells.get(k, 1e9), timed(lambda: ucall(k)))
+        for k in libs:
+            assert ucall(k) == 0
+        torch.cuda.synchronize()
+        (ra, sa), (rb, sb) = un["nr"], un["ieee"]
+        okr = (sb == 0)
+        rel_ray = ((ra[okr] - rb[okr]).abs().max()).item()  # unit rays: absolute = relative
+        print(json.dumps({"what": "unprojection: rcp/rsq+Newton tail vs IEEE div/sqrt",
+                          "model": mid, "points": n,
+                          "ms": {k: round(v, 4) for k, v in ucells.items()},
+                          "status_identical": bool(torch.equal(sa, sb)),
+                          "max_abs_ray_diff": rel_ray}), flush=True)
 
 
 if __name__ == "__main__":
