@@ -17,11 +17,14 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module doc)
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libacm.so")
+# ACM_LIB_PATH: load another build of the same C-ABI (the tools' diagnostic
+# and A/B builds, e.g. lib/libacm_ieee.so); default: the in-tree libacm.so
+LIB_PATH = os.environ.get("ACM_LIB_PATH") or os.path.join(_PKG_ROOT, "lib", "libacm.so")
 
 # model ids / codes (include/acm.h)
 PINHOLE, RADTAN, KANNALA_BRANDT, DOUBLE_SPHERE, UCM, EUCM, FOV = range(7)
 LAYOUT_AOS, LAYOUT_SOA = 0, 1
+EXACT_MATH = 0x100  # OR-ed into acm_project's layout (include/acm.h)
 INVALID_SKIP, INVALID_SENTINEL = 0, 1
 MAX_PARAMS = 9
 
@@ -64,7 +67,7 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
                                 ctypes.c_void_p)
 TUNE_PROJECT_VARIANT, TUNE_RESIDUAL_NT, TUNE_NE_WAVES, TUNE_FOV_UNROLL, TUNE_NE_UNROLL = 0, 1, 2, 3, 4
 TUNE_ALIGN_J, TUNE_NT_LOADS, TUNE_NT_LOADS_UNPROJECT, TUNE_LM_HOST_RESULT = 5, 6, 7, 8
-TUNE_SAMPLE_FUSED, TUNE_UNPROJECT_RCP = 9, 10
+TUNE_SAMPLE_FUSED, TUNE_UNPROJECT_RCP, TUNE_SAMPLE_PATIENCE = 9, 10, 11
 ERR_NOT_SUPPORTED = -6
 ERR_NUMERICAL = -7
 LM_TERMINATION = {0: "MaxIterations", 1: "CostTolerance", 2: "ParameterTolerance",

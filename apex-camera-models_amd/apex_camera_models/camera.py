@@ -203,7 +203,7 @@ class CameraModel:
 
     # --- batched drop-in (device tensors) --------------------------------
     def project_batch(self, points_3d, jacobian: bool = False, layout: str = "aos",
-                      out: Optional[Tuple[torch.Tensor, ...]] = None):
+                      out: Optional[Tuple[torch.Tensor, ...]] = None, exact: bool = False):
         """Batched `CameraModel::project` (mod.rs:256) (+ dense 2N x P Jacobian).
 
         points_3d: (N,3) float64 on the GPU (AoS, = nalgebra Matrix3xX) or, with
@@ -211,6 +211,7 @@ class CameraModel:
         jac is (P,N,2) -- memory identical to a 2N x P column-major DMatrix --
         or None.  Failed points: uv = NaN, J = 0, status = error code.
         A float32 input tensor selects the f32 kernels (acm_project_f32).
+        exact=True: ACM_EXACT_MATH (reference-exact KB / FOV math, include/acm.h).
         """
         lay = _lib.LAYOUT_SOA if layout == "soa" else _lib.LAYOUT_AOS
         pts = points_3d if isinstance(points_3d, torch.Tensor) else torch.as_tensor(
@@ -232,6 +233,8 @@ class CameraModel:
                    if jacobian else None)
         cam = self.acm_camera()
         fn = _lib.load().acm_project_f32 if dt == torch.float32 else _lib.load().acm_project
+        if exact and dt == torch.float64:
+            lay |= _lib.EXACT_MATH
         _lib.check(fn(ctypes.byref(cam), n, pts.data_ptr(), lay, uv.data_ptr(), st.data_ptr(),
                       jac.data_ptr() if jac is not None else None, _stream_handle()))
         return uv, st, jac
@@ -450,6 +453,11 @@ class FovModel(CameraModel):
 
     def _distortion_params(self):
         return [self.w]
+
+    def validate_params(self):  # fov.rs:457-468
+        super().validate_params()
+        if not math.isfinite(self.w) or self.w <= 2.220446049250313e-16 or self.w > 3.0:
+            raise InvalidParams(f"w must be in range (epsilon, 3.0], got {self.w}")
 
 
 MODEL_CLASSES = {

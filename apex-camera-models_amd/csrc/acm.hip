@@ -17,6 +17,8 @@
 //     result is bit-reproducible run to run.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
@@ -185,51 +187,58 @@ __device__ __forceinline__ void st1(uint8_t* p, uint8_t v) {
 // go to k_project_al unless ACM_TUNE_ALIGN_J = 0.)  A two-points-per-lane
 // variant measured no gain and was dropped.
 enum { kVarNT = 1, kVarGrid = 2, kVarNTL = 4 };
-static int g_project_variant = -1;
+static std::atomic<int> g_project_variant{-1};
 // Residual+J: plain stores by default.  Unlike project+J, non-temporal stores
 // measured slower here (DS, 9.3M points: 0.273 ms plain vs 0.310 ms nt,
 // profiles/r01_configs.log); -1 = auto (nt above kNtThresholdBytes), 1 = on.
-static int g_residual_nt = 0;
+static std::atomic<int> g_residual_nt{0};
 // Normal equations: minimum waves per SIMD for the register allocator (1, 3,
 // 4) and points per lane step (1, 2, 4); 0 = the per-model default below.
-static int g_ne_waves = 0;
-static int g_ne_unroll = 0;
+static std::atomic<int> g_ne_waves{0};
+static std::atomic<int> g_ne_unroll{0};
 // +J launches: -1 = auto = k_project_al (line-aligned store windows; as fast
 // as k_project for N a multiple of 8 and 30-45% faster otherwise,
 // profiles/r01_diag_align.log), 0 = k_project / k_residual, 1 = k_project_al.
-static int g_align_j = -1;
+static std::atomic<int> g_align_j{-1};
 // Non-temporal loads of the read-once point / observation streams in
 // k_normal_eq: -1 = auto (on), 0 = off, 1 = on (5-11% faster, read probe
 // 6.9 vs 6.3 TB/s; profiles/r01_ne_sweep.log, r01_hbm_ceiling.log).
-static int g_nt_loads = -1;
+static std::atomic<int> g_nt_loads{-1};
 // Non-temporal loads of the pixel stream in k_unproject (-1 auto = off, 0,
 // 1): beside the non-temporal ray stores they measured 2-25% slower for
 // every model (profiles/r01_diag_ntl.log).
-static int g_nt_loads_unproject = -1;
+static std::atomic<int> g_nt_loads_unproject{-1};
 // FOV grid search: points per lane step (1 = default, 2, 4).
-static int g_fov_unroll = 1;
+static std::atomic<int> g_fov_unroll{1};
 // sample_points: -1 = auto = single pass with decoupled look-back and the
 // per-model tile (SampleR), 0 = the two-pass count / scan / write path,
 // 1 / 2 / 3 = single pass with tiles of 4 / 8 / 16 x 256 cells.
-static int g_sample_fused = -1;
+static std::atomic<int> g_sample_fused{-1};
+// sample_points look-back: polls of an unpublished predecessor's status word
+// before the waiting wave counts that tile's cells itself (-1 = auto =
+// kLbPatience; 0 = at once, which exercises the fallback in tests).
+static std::atomic<int> g_sample_patience{-1};
 // Unprojections: (u - cx) / fx and (v - cy) / fy from the host's RN(1 / fx),
 // RN(1 / fy) (div_by_f, bit-identical) instead of two IEEE divisions per
 // point: -1 = auto = on, 0 = off, 1 = on.
-static int g_unproject_rcp = -1;
+static std::atomic<int> g_unproject_rcp{-1};
 // acm_lm_optimize without an all-reduce: the normal-equations epilogue writes
 // its P*P + P + 2 results straight into pinned host memory instead of device
 // memory + a device-to-host copy.  0 = off (copy + stream synchronise), 1 =
 // pinned results + stream synchronise, 2 = pinned results + the host spins
 // on a completion word the epilogue publishes; -1 = auto = 2.
-static int g_lm_host_result = -1;
-int lm_host_result() { return g_lm_host_result < 0 ? 2 : g_lm_host_result; }
+static std::atomic<int> g_lm_host_result{-1};
+int lm_host_result() {
+    const int v = g_lm_host_result.load(std::memory_order_relaxed);
+    return v < 0 ? 2 : v;
+}
 // Outputs above this many bytes are stored non-temporally.  Measured at 10M
 // points (profiles/r01_diag_ntl.log): project without J (170 MB out) 0.056 ms
 // nt vs 0.072 plain; a consumer that re-reads a smaller output soon after
 // still finds it in the 256 MiB Infinity Cache with plain stores.
 constexpr size_t kNtThresholdBytes = 64ull << 20;
 
-template <class TagT, int LAYOUT, bool WJ, bool NT>
+template <class TagT, int LAYOUT, bool WJ, bool NT, bool EXACT = false>
 __device__ __forceinline__ void project_point(const Cam<double>& c, size_t n, size_t i, double x,
                                               double y, double z, double* __restrict__ uv,
                                               uint8_t* __restrict__ status,
@@ -237,7 +246,7 @@ __device__ __forceinline__ void project_point(const Cam<double>& c, size_t n, si
     using M = typename TagT::template type<double>;
     constexpr int P = M::P;
     double u, v, ju[P], jv[P];
-    const uint8_t st = M::template project<WJ>(c, x, y, z, u, v, ju, jv);
+    const uint8_t st = M::template project<WJ, false, EXACT>(c, x, y, z, u, v, ju, jv);
     const bool ok = st == ST_OK;
     st2<NT>(uv + 2 * i, ok ? u : __builtin_nan(""), ok ? v : __builtin_nan(""));
     st1<NT>(status + i, st);
@@ -271,6 +280,24 @@ __global__ __launch_bounds__(kBlock) void k_project(acm_camera cam, size_t n,
         load_point<LAYOUT, NTL>(pts, n, i, x, y, z);
         project_point<TagT, LAYOUT, WJ, NT>(c, n, i, x, y, z, uv, status, jac);
     }
+}
+
+// ACM_EXACT_MATH projections of KB / FOV (camera_models.hpp EXACT: IEEE
+// sqrt / divisions and the double-double atan2): one point per lane, direct
+// stores.  Not a throughput path (the double-double atan2 costs ~10x the
+// polynomial); the other models are exact in every kernel.
+template <class TagT, int LAYOUT, bool WJ>
+__global__ __launch_bounds__(kBlock) void k_project_exact(acm_camera cam, size_t n,
+                                                          const double* __restrict__ pts,
+                                                          double* __restrict__ uv,
+                                                          uint8_t* __restrict__ status,
+                                                          double* __restrict__ jac) {
+    const Cam<double> c = make_cam<double>(cam);
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    double x, y, z;
+    load_point<LAYOUT>(pts, n, i, x, y, z);
+    project_point<TagT, LAYOUT, WJ, false, true>(c, n, i, x, y, z, uv, status, jac);
 }
 
 // ------------------------------------------------ project (+J), f32 sweep
@@ -1035,17 +1062,33 @@ struct Grid {
     uint32_t ncx, ncy;
     double cw, ch;
     size_t cell0;  // first cell of this launch (row-range shards, see acm_sample_points_range)
+    int patience;  // look-back polls before counting a predecessor's cells itself
+};
+
+// Row/column of a cell, advanced incrementally: one 64-bit division per lane
+// per workgroup (at the first cell it visits), then each step of kBlock cells
+// is an add and (for ncx >= kBlock) at most one wrap -- instead of a 64-bit
+// division and remainder (a ~50-instruction VALU sequence) per cell.
+struct CellWalk {
+    uint32_t i, j;
+    __device__ __forceinline__ void init(const Grid& g, size_t cell) {
+        cell += g.cell0;
+        i = (uint32_t)(cell / g.ncx);
+        j = (uint32_t)(cell - (size_t)i * g.ncx);
+    }
+    __device__ __forceinline__ void step(const Grid& g) {
+        j += kBlock;
+        while (j >= g.ncx) { j -= g.ncx; ++i; }
+    }
 };
 
 template <class TagT>
-__device__ __forceinline__ bool sample_cell(const Cam<double>& c, const Grid& g, size_t cell,
+__device__ __forceinline__ bool sample_cell(const Cam<double>& c, const Grid& g, const CellWalk& w,
                                             double& u, double& v, double& X, double& Y,
                                             double& Z) {
     using M = typename TagT::template type<double>;
-    cell += g.cell0;
-    const uint32_t i = (uint32_t)(cell / g.ncx), j = (uint32_t)(cell % g.ncx);
-    u = ((double)j + 0.5) * g.cw;  // :69
-    v = ((double)i + 0.5) * g.ch;  // :70
+    u = ((double)w.j + 0.5) * g.cw;  // :69
+    v = ((double)w.i + 0.5) * g.ch;  // :70
     const uint8_t st = M::unproject(c, u, v, X, Y, Z);
     return st == ST_OK && Z > 0.0;  // :91-94
 }
@@ -1063,11 +1106,13 @@ __global__ __launch_bounds__(kBlock) void k_sample_count(CamArg cam, Grid g, siz
     const Cam<double> c = make_cam<double>(cam);
     const size_t base = (size_t)blockIdx.x * kSampleCells;
     uint32_t mine = 0;
-    for (int r = 0; r < kSampleR; ++r) {
+    CellWalk cw;
+    cw.init(g, base + threadIdx.x);
+    for (int r = 0; r < kSampleR; ++r, cw.step(g)) {
         const size_t cell = base + (size_t)r * kBlock + threadIdx.x;
         if (cell < cells) {
             double u, v, X, Y, Z;
-            mine += sample_cell<TagT>(c, g, cell, u, v, X, Y, Z) ? 1u : 0u;
+            mine += sample_cell<TagT>(c, g, cw, u, v, X, Y, Z) ? 1u : 0u;
         }
     }
     __shared__ uint32_t sm[kBlock / 64];
@@ -1127,11 +1172,13 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(CamArg cam, Grid g, siz
     __shared__ uint32_t sm[kBlock / 64];
     const size_t base = (size_t)blockIdx.x * kSampleCells;
     uint64_t run = offsets[blockIdx.x];
-    for (int r = 0; r < kSampleR; ++r) {
+    CellWalk cw;
+    cw.init(g, base + threadIdx.x);
+    for (int r = 0; r < kSampleR; ++r, cw.step(g)) {
         const size_t cell = base + (size_t)r * kBlock + threadIdx.x;
         bool keep = false;
         double u = 0, v = 0, X = 0, Y = 0, Z = 0;
-        if (cell < cells) keep = sample_cell<TagT>(c, g, cell, u, v, X, Y, Z);
+        if (cell < cells) keep = sample_cell<TagT>(c, g, cw, u, v, X, Y, Z);
         const uint64_t m = __ballot(keep);
         if (lane == 0) sm[wid] = (uint32_t)__popcll(m);
         __syncthreads();
@@ -1143,7 +1190,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(CamArg cam, Grid g, siz
         const uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
         if (keep) {
             const size_t k = wbase + (uint64_t)__popcll(below);
-            *reinterpret_cast<double2*>(uv_out + 2 * k) = make_double2(u, v);
+            st2<false>(uv_out + 2 * k, u, v);
             xyz_out[3 * k] = X;
             xyz_out[3 * k + 1] = Y;
             xyz_out[3 * k + 2] = Z;
@@ -1153,19 +1200,22 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(CamArg cam, Grid g, siz
     }
 }
 
-// Single pass (ACM_TUNE_SAMPLE_FUSED, default): each workgroup takes the
-// next tile of kFusedR x 256 cells from an atomic ticket, unprojects them
-// once keeping the rays in registers, publishes its kept count, and finds
-// its output offset by a decoupled look-back over the tiles before it (one
-// status word per tile: flag in bits 62-63 -- 1 = count of this tile only,
-// 2 = inclusive prefix -- and the count below).  Wave 0 inspects 64
-// predecessors per load.  The ticket order makes every predecessor a
-// workgroup that is already running, and a running workgroup publishes its
-// count without waiting on anything, so the look-back always terminates.
-// The kept points come out in cell order exactly as from the two-pass path.
+// Single pass (ACM_TUNE_SAMPLE_FUSED, default): workgroup b owns tile b of
+// kFusedR x 256 cells, unprojects them once keeping the rays in registers,
+// publishes its kept count, and finds its output offset by a decoupled
+// look-back over the tiles before it (one status word per tile: flag in bits
+// 62-63 -- 1 = count of this tile only, 2 = inclusive prefix -- and the count
+// below).  Wave 0 inspects 64 predecessors per load.  No ticket atomic: the
+// 48.8K same-address returning atomics of a 1e8-cell grid alone took 0.37 ms
+// (profiles/r02_diag_sample_phases.log), and the look-back does not need them
+// for progress -- a predecessor that has not published after kLbPatience
+// polls (one that is not resident: the dispatch order is not guaranteed) has
+// its count computed by the waiting wave itself (tile_keep_count), so no
+// workgroup ever waits on one that has not started.  The kept points come out
+// in cell order exactly as from the two-pass path.
 constexpr int kFusedRMin = 4;  // smallest tile (rounds of 256 cells) any setting uses
-// Per-model tile: fewer, larger tiles mean fewer same-address ticket atomics
-// and look-backs, more rays held in registers.  Fastest cell of the
+// Per-model tile: fewer, larger tiles mean fewer look-backs, more rays held
+// in registers.  Fastest cell of the
 // interleaved {4, 8, 16} x 256 sweep at 1e8 cells (profiles/r01s7_diag_sample.log).
 template <class TagT> struct SampleR { static constexpr int R = 8; };
 template <> struct SampleR<Tag<Pinhole>> { static constexpr int R = 16; };
@@ -1173,99 +1223,205 @@ template <> struct SampleR<Tag<Ucm>> { static constexpr int R = 16; };
 template <> struct SampleR<Tag<Eucm>> { static constexpr int R = 16; };
 constexpr size_t kFusedCells = (size_t)kBlock * kFusedRMin;
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
+constexpr int kLbPatience = 512;  // polls (s_sleep between) before computing a count itself
 
 template <class TagT, int kFusedR>
 __global__ __launch_bounds__(kBlock) void k_sample_fused(CamArg cam, Grid g, size_t cells,
-                                                         uint64_t* __restrict__ ticket,
                                                          uint64_t* __restrict__ status,
                                                          double* __restrict__ uv_out,
                                                          double* __restrict__ xyz_out,
                                                          uint64_t* __restrict__ out_counts) {
     const Cam<double> c = make_cam<double>(cam);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    __shared__ uint64_t s_tile, s_excl;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+    __shared__ uint64_t s_excl;
     __shared__ uint32_t sm[kFusedR][kBlock / 64];
-    if (threadIdx.x == 0) s_tile = atomicAdd((unsigned long long*)ticket, 1ull);
-    __syncthreads();
-    const uint64_t tile = s_tile;
+    __shared__ double s_xyz[kBlock / 64][64 * 3];  // per-wave store staging (6 KiB)
+    // look-back state that survives the workgroup-wide fallback rounds
+    __shared__ uint64_t s_lb_top, s_lb_excl, s_lb_helped, s_lb_help;
+    __shared__ uint64_t s_lb_val[64];
+    __shared__ uint32_t s_lb_cnt[kBlock / 64];
+    __shared__ int s_lb_state;
+    const uint64_t tile = blockIdx.x;
     constexpr size_t kTile = (size_t)kBlock * kFusedR;
     const size_t base = (size_t)tile * kTile;
     double X[kFusedR], Y[kFusedR], Z[kFusedR];
     uint64_t m[kFusedR];
-#pragma unroll
-    for (int r = 0; r < kFusedR; ++r) {
-        const size_t cell = base + (size_t)r * kBlock + threadIdx.x;
-        bool keep = false;
-        double u, v;
-        X[r] = Y[r] = Z[r] = 0.0;
-        if (cell < cells) keep = sample_cell<TagT>(c, g, cell, u, v, X[r], Y[r], Z[r]);
-        m[r] = __ballot(keep);
-        if (lane == 0) sm[r][wid] = (uint32_t)__popcll(m[r]);
+    if (threadIdx.x == 0) {
+        s_lb_top = tile - 1;  // lane l of wave 0 inspects tile top - l
+        s_lb_excl = 0;
+        s_lb_helped = 0;
+        s_lb_state = tile == 0 ? 1 : 0;
     }
-    __syncthreads();
-    if (wid == 0) {
-        uint64_t agg = 0;
+    // One compute block serves this tile and, on the rare fallback path, a
+    // predecessor whose count the look-back could not get (a second inlined
+    // unprojection beside the live rays cost 50 VGPRs).  `work` is the tile
+    // whose rays and counts the registers / sm hold.
+    uint64_t work = tile;
+    uint64_t agg = 0;
+    bool published = false;
+#if ACM_DIAG_SAMPLE == 5  // experiment: stagger the first resident batch over ~one tile time
+    if (blockIdx.x < 2048u) {
+        const int k = (int)(blockIdx.x * 7u % 16u);
+        for (int i = 0; i < k; ++i) __builtin_amdgcn_s_sleep(41);
+    }
+#endif
+    for (;;) {
+        const size_t wbase0 = (size_t)work * kTile;
+        CellWalk cw;
+        cw.init(g, wbase0 + threadIdx.x);
+#pragma unroll
+        for (int r = 0; r < kFusedR; ++r, cw.step(g)) {
+            const size_t cell = wbase0 + (size_t)r * kBlock + threadIdx.x;
+            bool keep = false;
+            double u, v;
+            X[r] = Y[r] = Z[r] = 0.0;
+#if ACM_DIAG_SAMPLE == 2 || ACM_DIAG_SAMPLE == 3  // diagnostic builds: no unprojection
+            u = ((double)cw.j + 0.5) * g.cw;
+            v = ((double)cw.i + 0.5) * g.ch;
+            X[r] = u; Y[r] = v; Z[r] = 1.0;
+            keep = cell < cells && (cw.i + cw.j) % 16 != 0;
+#else
+            if (cell < cells) keep = sample_cell<TagT>(c, g, cw, u, v, X[r], Y[r], Z[r]);
+#endif
+            m[r] = __ballot(keep);
+            if (lane == 0) sm[r][wid] = (uint32_t)__popcll(m[r]);
+        }
+        __syncthreads();
+        uint64_t cnt = 0;
         for (int r = 0; r < kFusedR; ++r)
-            for (int w = 0; w < kBlock / 64; ++w) agg += sm[r][w];
-        if (lane == 0)
-            __hip_atomic_store(status + tile, (tile == 0 ? kLbIncl : kLbAgg) | agg,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t excl = 0;
-        if (tile > 0) {
-            int64_t top = (int64_t)tile - 1;  // lane l inspects tile top - l
-            for (;;) {
+            for (int w = 0; w < kBlock / 64; ++w) cnt += sm[r][w];
+        if (work == tile) {
+            agg = cnt;
+            if (!published && threadIdx.x == 0)
+                __hip_atomic_store(status + tile, (tile == 0 ? kLbIncl : kLbAgg) | agg,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            published = true;
+        } else if (threadIdx.x == 0) {  // a helped predecessor: its count joins the window
+            const uint64_t l = s_lb_help;
+            s_lb_val[l] = kLbAgg | cnt;
+            s_lb_helped |= 1ull << l;
+        }
+        __syncthreads();
+        // Decoupled look-back by wave 0.  A predecessor that has not
+        // published after g.patience polls is counted here by the whole
+        // workgroup (next pass of the loop); then this tile is recomputed.
+        if (wid == 0 && __builtin_amdgcn_readfirstlane(s_lb_state) == 0) {
+            int64_t top = (int64_t)s_lb_top;
+            uint64_t excl = s_lb_excl, helped = s_lb_helped;
+            const uint64_t help_w = ((helped >> lane) & 1ull) ? s_lb_val[lane] : 0;
+            for (int polls = 0;;) {
                 const int64_t idx = top - lane;
-                const uint64_t w = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT)
-                                            : kLbIncl;  // before tile 0: prefix 0
+                uint64_t w = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : kLbIncl;  // before tile 0: prefix 0
+                if (((helped >> lane) & 1ull) && (w >> 62) == 0) w = help_w;
                 const uint64_t incl = __ballot((w >> 62) == 2);
                 const uint64_t none = __ballot((w >> 62) == 0);
                 const int stop = incl ? __ffsll((long long)incl) - 1 : 64;
                 const uint64_t need = stop == 63 || stop == 64 ? ~0ull : ((2ull << stop) - 1);
                 if (none & need) {  // a nearer tile has not published yet
-                    __builtin_amdgcn_s_sleep(2);
-                    continue;
+                    if (++polls < g.patience) {
+                        __builtin_amdgcn_s_sleep(2);
+                        continue;
+                    }
+                    if (lane == 0) {  // not resident (or very late): count it here
+                        s_lb_top = (uint64_t)top;
+                        s_lb_excl = excl;
+                        s_lb_help = (uint64_t)(__ffsll((long long)(none & need)) - 1);
+                        s_lb_state = 2;
+                    }
+                    break;
                 }
                 uint64_t v = lane <= stop ? (w & kLbVal) : 0;
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
                 excl += v;
-                if (stop < 64) break;
+                if (stop < 64) {
+                    if (lane == 0) {
+                        __hip_atomic_store(status + tile, kLbIncl | (excl + agg),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        s_lb_excl = excl;
+                        s_lb_state = 1;
+                    }
+                    break;
+                }
                 top -= 64;
+                helped = 0;
+                polls = 0;
             }
-            if (lane == 0)
-                __hip_atomic_store(status + tile, kLbIncl | (excl + agg), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (lane == 0) {
-            s_excl = excl;
-            if (base + kTile >= cells) {  // last tile: the kept total
-                out_counts[0] = excl + agg;
-                out_counts[1] = cells;
-            }
+        __syncthreads();
+        const int state = __builtin_amdgcn_readfirstlane(s_lb_state);
+        if (state == 1 && work == tile) break;  // prefix known, own rays in registers
+        if (state == 2) {
+            work = s_lb_top - s_lb_help;
+            __syncthreads();  // everyone has read the request before it is reset
+            if (threadIdx.x == 0) s_lb_state = 0;
+        } else {
+            work = tile;  // prefix known: recompute this tile's rays
+        }
+    }
+    if (threadIdx.x == 0) {
+        s_excl = s_lb_excl;
+        if (base + kTile >= cells) {  // last tile: the kept total
+            out_counts[0] = s_lb_excl + agg;
+            out_counts[1] = cells;
         }
     }
     __syncthreads();
     uint64_t run = s_excl;
     const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
+    double* lx = s_xyz[wid];
+    CellWalk cw;
+    cw.init(g, base + threadIdx.x);
 #pragma unroll
-    for (int r = 0; r < kFusedR; ++r) {
+    for (int r = 0; r < kFusedR; ++r, cw.step(g)) {
         uint64_t wbase = run, tot = 0;
         for (int w = 0; w < kBlock / 64; ++w) {
             if (w < wid) wbase += sm[r][w];
             tot += sm[r][w];
         }
+        const uint32_t rank = (uint32_t)__popcll(m[r] & below);
+        const uint32_t cnt = (uint32_t)__popcll(m[r]);
+#if ACM_DIAG_SAMPLE == 1 || ACM_DIAG_SAMPLE == 3  // diagnostic builds: no output stores
+        if (((m[r] >> lane) & 1ull) && X[r] == 1234.5) {
+#else
         if ((m[r] >> lane) & 1ull) {
-            const size_t cell = base + (size_t)r * kBlock + threadIdx.x + g.cell0;
-            const uint32_t i = (uint32_t)(cell / g.ncx), j = (uint32_t)(cell % g.ncx);
-            const size_t k = wbase + (uint64_t)__popcll(m[r] & below);
-            // the same u, v as sample_cell (point_sampling.rs:69-70)
-            *reinterpret_cast<double2*>(uv_out + 2 * k) =
-                make_double2(((double)j + 0.5) * g.cw, ((double)i + 0.5) * g.ch);
-            xyz_out[3 * k] = X[r];
-            xyz_out[3 * k + 1] = Y[r];
-            xyz_out[3 * k + 2] = Z[r];
+#endif
+            // the same u, v as sample_cell (point_sampling.rs:69-70): 16 B per
+            // lane, consecutive kept points -> one contiguous run per wave
+            st2<false>(uv_out + 2 * (wbase + rank), ((double)cw.j + 0.5) * g.cw,
+                       ((double)cw.i + 0.5) * g.ch);
+            lx[3 * rank] = X[r];
+            lx[3 * rank + 1] = Y[r];
+            lx[3 * rank + 2] = Z[r];
         }
+        // The wave's kept rays are 3*cnt consecutive doubles of xyz_out: written
+        // from the wave's LDS slab as 16-B pieces on the 16-B grid (plus a single
+        // leading / trailing double) instead of three 8-B stores per lane at a
+        // 24-B stride.  LDS accesses of one wave complete in order; the fences
+        // keep the compiler from moving the reads above the writes.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if ACM_DIAG_SAMPLE != 1 && ACM_DIAG_SAMPLE != 3
+        if (cnt) {
+            double* dst = xyz_out + 3 * wbase;
+            const uint32_t nd = 3 * cnt;
+            const uint32_t h = (uint32_t)((reinterpret_cast<uintptr_t>(dst) >> 3) & 1u);
+            const uint32_t np = (nd - h) >> 1;
+            for (uint32_t p = lane; p < np; p += 64) {
+                const uint32_t d = h + 2 * p;
+                st2<false>(dst + d, lx[d], lx[d + 1]);
+            }
+            if (lane == 0 && h) dst[0] = lx[0];
+            if (lane == 63 && ((nd - h) & 1u)) dst[nd - 1] = lx[nd - 1];
+        }
+#endif
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the slab is rewritten next round
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         run += tot;
     }
 }
@@ -1882,7 +2038,11 @@ __global__ __launch_bounds__(kBlock) void k_undistort(acm_camera cam, double tfx
     const double x_norm = ((double)u_out - tcx) / tfx;  // :35-36
     const double y_norm = ((double)v_out - tcy) / tfy;
     double su, sv;
-    const uint8_t st = M::template project<false>(c, x_norm, y_norm, 1.0, su, sv, nullptr, nullptr);
+    // EXACT: the source coordinate is quantised by round() / floor() below,
+    // so it takes the reference-exact projection (IEEE sqrt / divisions and
+    // the correctly rounded atan2 for KB / FOV; camera_models.hpp)
+    const uint8_t st =
+        M::template project<false, false, true>(c, x_norm, y_norm, 1.0, su, sv, nullptr, nullptr);
     uint8_t r = 0, g = 0, b = 0;
     if (st == ST_OK) {
         if (!BILINEAR) {  // :61-69
@@ -1999,6 +2159,10 @@ ACM_API int acm_validate_params(const acm_camera* cam) {
         if (!std::isfinite(p[4])) return fail(ACM_INVALID_DISTORTION, "alpha must be finite");
         if (!std::isfinite(p[5])) return fail(ACM_INVALID_DISTORTION, "beta must be finite");
         break;
+    case ACM_FOV:  // fov.rs:457-468
+        if (!std::isfinite(p[4]) || p[4] <= kEps || p[4] > 3.0)
+            return fail(ACM_INVALID_DISTORTION, "w must be in range (epsilon, 3.0]");
+        break;
     default: break;
     }
     return ACM_VALID;
@@ -2029,10 +2193,28 @@ ACM_API int acm_project(const acm_camera* cam, size_t n, const double* points_3d
                         double* points_2d, uint8_t* status, double* jacobian, void* stream) {
     int rc = check_cam(cam);
     if (rc) return rc;
+    const bool exact = (layout & ACM_EXACT_MATH) != 0;
+    layout &= ~ACM_EXACT_MATH;
     if ((rc = check_layout(layout))) return rc;
     if (n == 0) return ACM_SUCCESS;
     if (!points_3d || !points_2d || !status) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
     hipStream_t s = (hipStream_t)stream;
+    if (exact && (cam->model == ACM_KANNALA_BRANDT || cam->model == ACM_FOV)) {
+        return dispatch_model(cam->model, [&](auto tag) -> int {
+            using TagT = decltype(tag);
+            const dim3 g(grid_for(n)), b(kBlock);
+#define ACM_EX(L, WJ)                                                                          \
+    hipLaunchKernelGGL((k_project_exact<TagT, L, WJ>), g, b, 0, s, prep(*cam), n, points_3d,     \
+                       points_2d, status, jacobian)
+            if (layout == ACM_LAYOUT_AOS) {
+                if (jacobian) ACM_EX(ACM_LAYOUT_AOS, true); else ACM_EX(ACM_LAYOUT_AOS, false);
+            } else {
+                if (jacobian) ACM_EX(ACM_LAYOUT_SOA, true); else ACM_EX(ACM_LAYOUT_SOA, false);
+            }
+#undef ACM_EX
+            return check_launch("acm_project (exact math)");
+        });
+    }
     int var = g_project_variant;
     if (var < 0) {
         const size_t out_bytes =
@@ -2227,8 +2409,9 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
         double* parts = (double*)workspace;
         int nb = nb_max;
         using Def = NeDefault<TagT>;
-        const int wv = g_ne_waves ? g_ne_waves : Def::W;
-        const int un = g_ne_unroll ? g_ne_unroll : Def::U;
+        const int wv0 = g_ne_waves, un0 = g_ne_unroll;
+        const int wv = wv0 ? wv0 : Def::W;
+        const int un = un0 ? un0 : Def::U;
         auto go = [&](auto lay_c, auto w_c) {
             constexpr int LAY = decltype(lay_c)::value, W = decltype(w_c)::value;
             const bool ntl = g_nt_loads != 0;
@@ -2325,7 +2508,8 @@ ACM_API int acm_sample_points_grid(uint32_t width, uint32_t height, size_t n_req
 }
 
 // two-pass: counts + offsets (2 per kSampleCells tile); single pass: one
-// status word per kFusedCells tile + the ticket
+// status word per kFusedCells tile (+ one word, formerly a ticket, kept so
+// the workspace size is unchanged)
 static size_t sample_ws_words(size_t cells) {
     const size_t nb = cells ? (cells + kSampleCells - 1) / kSampleCells : 1;
     const size_t nt = cells ? (cells + kFusedCells - 1) / kFusedCells : 1;
@@ -2364,10 +2548,14 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
     g.cw = (double)cam->width / (double)ncx;  // point_sampling.rs:57
     g.ch = (double)cam->height / (double)ncy;
     g.cell0 = cell_begin;
+    const int pat = g_sample_patience;
+    g.patience = pat < 0 ? kLbPatience : pat;
     hipStream_t s = (hipStream_t)stream;
-    if (g_sample_fused != 0) {
-        uint64_t* ticket = (uint64_t*)workspace;
-        uint64_t* status = ticket + 1;
+    // (plain stores: non-temporal ones measured slower for these compacted
+    // outputs, 1.41 -> 1.47 ms at 1e8 KB cells, profiles/r02_diag_sample_phases.log)
+    const int fused = g_sample_fused;
+    if (fused != 0) {
+        uint64_t* status = (uint64_t*)workspace + 1;
         if (hipMemsetAsync(workspace, 0, (nt + 1) * sizeof(uint64_t), s) != hipSuccess)
             return check_launch("acm_sample_points: workspace clear");
         if (!cells) {  // no tile runs: counts = [0 kept, 0 cells]
@@ -2377,16 +2565,13 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
         }
         return dispatch_model(cam->model, [&](auto tag) -> int {
             using TagT = decltype(tag);
-            const int rr = g_sample_fused == 1   ? 4
-                           : g_sample_fused == 2 ? 8
-                           : g_sample_fused == 3 ? 16
-                                                 : SampleR<TagT>::R;
+            const int rr = fused == 1 ? 4 : fused == 2 ? 8 : fused == 3 ? 16 : SampleR<TagT>::R;
             const size_t ntr = (cells + (size_t)kBlock * rr - 1) / ((size_t)kBlock * rr);
             auto kern = k_sample_fused<TagT, 4>;
             if (rr == 8) kern = k_sample_fused<TagT, 8>;
             if (rr == 16) kern = k_sample_fused<TagT, 16>;
             hipLaunchKernelGGL(kern, dim3((unsigned)ntr), dim3(kBlock), 0, s, prep(*cam), g, cells,
-                               ticket, status, points_2d_out, points_3d_out, counts);
+                               status, points_2d_out, points_3d_out, counts);
             return check_launch("acm_sample_points");
         });
     }
@@ -2398,8 +2583,8 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
                            g, cells, cnt);
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, cnt, nb, off, counts,
                            (uint64_t)cells);
-        hipLaunchKernelGGL((k_sample_write<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, prep(*cam),
-                           g, cells, off, points_2d_out, points_3d_out);
+        hipLaunchKernelGGL((k_sample_write<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s,
+                           prep(*cam), g, cells, off, points_2d_out, points_3d_out);
         return check_launch("acm_sample_points");
     });
 }
@@ -2668,75 +2853,37 @@ ACM_API int acm_stream_synchronize(void* stream) {
 }
 
 ACM_API int acm_set_tuning(int key, int value) {
-    if (key == ACM_TUNE_PROJECT_VARIANT) {
-        if (value < -1 || value > 7)
-            return fail(ACM_ERR_INVALID_ARGUMENT, "variant must be -1 (auto) or 0..7");
-        const int old = g_project_variant;
-        g_project_variant = value;
-        return old;
-    }
-    if (key == ACM_TUNE_RESIDUAL_NT) {
-        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
-        const int old = g_residual_nt;
-        g_residual_nt = value;
-        return old;
-    }
-    if (key == ACM_TUNE_NE_WAVES) {
-        if (value != 0 && value != 1 && value != 3 && value != 4)
-            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 0 (per-model default), 1, 3 or 4");
-        const int old = g_ne_waves;
-        g_ne_waves = value;
-        return old;
-    }
-    if (key == ACM_TUNE_NE_UNROLL) {
-        if (value < 0 || value > 3)
-            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 0 (per-model default), 1, 2 or 3");
-        const int old = g_ne_unroll;
-        g_ne_unroll = value;
-        return old;
-    }
-    if (key == ACM_TUNE_ALIGN_J) {
-        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
-        const int old = g_align_j;
-        g_align_j = value;
-        return old;
-    }
-    if (key == ACM_TUNE_NT_LOADS) {
-        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
-        const int old = g_nt_loads;
-        g_nt_loads = value;
-        return old;
-    }
-    if (key == ACM_TUNE_NT_LOADS_UNPROJECT) {
-        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
-        const int old = g_nt_loads_unproject;
-        g_nt_loads_unproject = value;
-        return old;
-    }
-    if (key == ACM_TUNE_LM_HOST_RESULT) {
-        if (value < -1 || value > 2) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..2");
-        const int old = g_lm_host_result;
-        g_lm_host_result = value;
-        return old;
-    }
-    if (key == ACM_TUNE_UNPROJECT_RCP) {
-        if (value < -1 || value > 1) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..1");
-        const int old = g_unproject_rcp;
-        g_unproject_rcp = value;
-        return old;
-    }
-    if (key == ACM_TUNE_SAMPLE_FUSED) {
-        if (value < -1 || value > 3) return fail(ACM_ERR_INVALID_ARGUMENT, "value must be -1..3");
-        const int old = g_sample_fused;
-        g_sample_fused = value;
-        return old;
-    }
-    if (key == ACM_TUNE_FOV_UNROLL) {
-        if (value != 1 && value != 2 && value != 4)
-            return fail(ACM_ERR_INVALID_ARGUMENT, "value must be 1, 2 or 4");
-        const int old = g_fov_unroll;
-        g_fov_unroll = value;
-        return old;
+    // Every knob is a std::atomic<int> read with one load per launch, so
+    // concurrent callers and concurrent acm_set_tuning calls are race-free
+    // (each launch sees either the old or the new value; results are
+    // identical for every setting).
+    struct Knob {
+        int key;
+        std::atomic<int>* v;
+        int lo, hi;
+        const char* msg;
+    };
+    static const Knob knobs[] = {
+        {ACM_TUNE_PROJECT_VARIANT, &g_project_variant, -1, 7, "variant must be -1 (auto) or 0..7"},
+        {ACM_TUNE_RESIDUAL_NT, &g_residual_nt, -1, 1, "value must be -1..1"},
+        {ACM_TUNE_NE_WAVES, &g_ne_waves, 0, 4, "value must be 0 (per-model default), 1, 3 or 4"},
+        {ACM_TUNE_FOV_UNROLL, &g_fov_unroll, 1, 4, "value must be 1, 2 or 4"},
+        {ACM_TUNE_NE_UNROLL, &g_ne_unroll, 0, 3, "value must be 0 (per-model default), 1, 2 or 3"},
+        {ACM_TUNE_ALIGN_J, &g_align_j, -1, 1, "value must be -1..1"},
+        {ACM_TUNE_NT_LOADS, &g_nt_loads, -1, 1, "value must be -1..1"},
+        {ACM_TUNE_NT_LOADS_UNPROJECT, &g_nt_loads_unproject, -1, 1, "value must be -1..1"},
+        {ACM_TUNE_LM_HOST_RESULT, &g_lm_host_result, -1, 2, "value must be -1..2"},
+        {ACM_TUNE_SAMPLE_FUSED, &g_sample_fused, -1, 3, "value must be -1..3"},
+        {ACM_TUNE_UNPROJECT_RCP, &g_unproject_rcp, -1, 1, "value must be -1..1"},
+        {ACM_TUNE_SAMPLE_PATIENCE, &g_sample_patience, -1, 1 << 20, "value must be -1..2^20"},
+    };
+    for (const Knob& k : knobs) {
+        if (k.key != key) continue;
+        bool ok = value >= k.lo && value <= k.hi;
+        if (key == ACM_TUNE_NE_WAVES) ok = ok && value != 2;
+        if (key == ACM_TUNE_FOV_UNROLL) ok = ok && value != 3;
+        if (!ok) return fail(ACM_ERR_INVALID_ARGUMENT, k.msg);
+        return k.v->exchange(value);
     }
     return fail(ACM_ERR_INVALID_ARGUMENT, "unknown tuning key");
 }

@@ -6,19 +6,39 @@
 // evaluates `a + b + c` as (a + b) + c and never contracts to FMA; this file
 // is compiled with -ffp-contract=off so hipcc does not either), which is what
 // makes the validity masks bit-exact: every threshold test sees the same
-// doubles as the reference.  Divisions and square roots are the IEEE
-// correctly-rounded f64 sequences hipcc emits by default (no -ffast-math).
-// Only atan2 (our polynomial, atan2_ge0) and sin/cos (OCML) can differ from
-// glibc by ulps, and no status decision depends on them.  Several divisions
-// by one divisor go through div_shared, bit-identical to dividing each.
+// doubles as the reference.
+//
+// Where the double path is NOT the reference's correctly rounded operation
+// sequence (every other division and square root is the IEEE sequence hipcc
+// emits by default, no -ffast-math):
+//   * KB project: atan2 is the polynomial atan2_ge0 (<= ~2 ulp from glibc),
+//     and r = sqrt(x^2+y^2), 1/r and the atan2 quotient come from
+//     v_rsq_f64 / v_rcp_f64 + two Newton steps (~1 ulp; rsq_nr, rcp_nr) for
+//     r^2, z in [2^-1000, 2^1000] (the IEEE forms outside; ACM_IEEE_MATH
+//     builds the IEEE forms everywhere).  The axis test r < EPS stays exact:
+//     only r^2 < 1e-30 can pass it and that case takes the IEEE sqrt.
+//   * KB unproject: sin / cos of the Newton angle are polynomials on [0, 2]
+//     (sincos_0_2, OCML beyond), and after the Newton loop 1/ru and 1/|p|
+//     come from rcp_nr / rsq_nr (the IEEE forms outside [2^-1000, 2^1000]).
+//     The Newton iterates and every status decision are the reference's.
+//   * FOV project: atan2 is atan2_ge0; FOV unproject: OCML sincos.
+//   * project<.., FAST = true> (the fused normal equations only): one
+//     reciprocal and products instead of the per-point divisions.
+// None of these feeds a status decision, so statuses are bit-exact
+// everywhere; values are held to 1e-10 relative (tests/test_gpu_parity.py,
+// observed ~1e-15).  project<.., EXACT = true> (acm_project with
+// ACM_EXACT_MATH, and undistort_image, whose bytes round() / floor() the
+// source coordinates) takes the IEEE sqrt / divisions and the correctly
+// rounded double-double atan2 of exact_math.hpp: KB and FOV projections and
+// Jacobians then equal the reference bit for bit wherever glibc's atan2 is
+// correctly rounded (all but ~0.2% of arguments; there they differ by one
+// ulp and ours is the correctly rounded one).  tests/test_gpu_exact.py pins
+// the EXACT path to the oracle and the fast path to the EXACT one.
+// Several divisions by one divisor go through div_shared, bit-identical to
+// dividing each.
 //
 // Status decisions are computed branch-free where possible so a wave does
 // not diverge on the rare failing point; the caller selects outputs.
-//
-// KB's projection (double) takes r, 1/r and its atan2 quotient from the
-// hardware rsq / rcp estimates + Newton steps (~1 ulp; ACM_IEEE_MATH builds
-// the IEEE sqrt / divisions instead): like its polynomial atan2 it is held
-// to 1e-10 against the reference, with the status decisions exact.
 //
 // project<WJ, FAST>: FAST = true (used only by the fused normal-equations
 // kernel, whose sums are held to 1e-10 anyway and are summed in a different
@@ -34,6 +54,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+
+#include "exact_math.hpp"
 
 namespace acm {
 
@@ -100,6 +122,15 @@ __device__ __forceinline__ double atan2_ge0(double y, double x) {
     return atan2(y, x);
 }
 __device__ __forceinline__ float atan2_ge0(float y, float x) { return atan2(y, x); }
+
+// The reference-exact atan2 (EXACT projections): the double-double,
+// correctly rounded atan2_cr of exact_math.hpp where it is defined (y >= 0,
+// x > 0, finite: every point whose status is Ok), OCML's atan2 elsewhere.
+__device__ __forceinline__ double atan2_exact(double y, double x) {
+    const double t = xm::atan2_cr(y, x);
+    return t == t ? t : atan2(y, x);
+}
+__device__ __forceinline__ float atan2_exact(float y, float x) { return atan2(y, x); }
 
 // 1/sqrt(a) and 1/a from the hardware estimates (v_rsq_f64 / v_rcp_f64)
 // with two Newton-Raphson steps each: within ~1 ulp for a in
@@ -241,7 +272,7 @@ template <class T>
 struct Pinhole {
     static constexpr int P = 4;
     // pinhole.rs:165-182
-    template <bool WJ, bool FAST = false>
+    template <bool WJ, bool FAST = false, bool EXACT = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
@@ -279,7 +310,7 @@ template <class T>
 struct RadTan {
     static constexpr int P = 9;  // fx fy cx cy k1 k2 p1 p2 k3
     // rad_tan.rs:302-348
-    template <bool WJ, bool FAST = false>
+    template <bool WJ, bool FAST = false, bool EXACT = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
@@ -380,7 +411,7 @@ template <class T>
 struct KannalaBrandt {
     static constexpr int P = 8;  // fx fy cx cy k1 k2 k3 k4
     // kannala_brandt.rs:340-394
-    template <bool WJ, bool FAST = false>
+    template <bool WJ, bool FAST = false, bool EXACT = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
@@ -391,7 +422,7 @@ struct KannalaBrandt {
         T r, theta, ir = T(0);
         bool axis;
 #ifndef ACM_IEEE_MATH
-        if constexpr (sizeof(T) == 8) {
+        if constexpr (sizeof(T) == 8 && !EXACT) {
             // r, 1/r and the atan2 quotient from rsq / rcp + Newton (~1 ulp;
             // the model is already held to 1e-10, not bit-exactness).  The
             // axis test r < EPS (:375) stays exact: only r2 < 1e-30 can pass
@@ -414,7 +445,7 @@ struct KannalaBrandt {
 #endif
         {
             r = sqrt(r2);
-            theta = atan2_ge0(r, z);  // :365 (r >= 0)
+            theta = EXACT ? atan2_exact(r, z) : atan2_ge0(r, z);  // :365 (r >= 0)
             axis = r < T(kEps);  // :375
             if (FAST) ir = T(1) / r;
         }
@@ -425,7 +456,7 @@ struct KannalaBrandt {
         T theta9 = theta7 * theta2;
         T theta_d = theta + k1 * theta3 + k2 * theta5 + k3 * theta7 + k4 * theta9;
 #ifndef ACM_IEEE_MATH
-        constexpr bool kMul = FAST || sizeof(T) == 8;
+        constexpr bool kMul = FAST || (sizeof(T) == 8 && !EXACT);
 #else
         constexpr bool kMul = FAST;
 #endif
@@ -520,7 +551,7 @@ template <class T>
 struct DoubleSphere {
     static constexpr int P = 6;  // fx fy cx cy alpha xi
     // double_sphere.rs:361-390 + check_projection_condition :177-184
-    template <bool WJ, bool FAST = false>
+    template <bool WJ, bool FAST = false, bool EXACT = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
@@ -584,7 +615,7 @@ template <class T>
 struct Ucm {
     static constexpr int P = 5;  // fx fy cx cy alpha
     // ucm.rs:297-316 + check_proj_condition :154-161
-    template <bool WJ, bool FAST = false>
+    template <bool WJ, bool FAST = false, bool EXACT = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], alpha = c.p[4];
@@ -635,7 +666,7 @@ template <class T>
 struct Eucm {
     static constexpr int P = 6;  // fx fy cx cy alpha beta
     // eucm.rs:328-347 + check_proj_condition :167-177
-    template <bool WJ, bool FAST = false>
+    template <bool WJ, bool FAST = false, bool EXACT = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
@@ -695,14 +726,15 @@ template <class T>
 struct Fov {
     static constexpr int P = 5;  // fx fy cx cy w
     // fov.rs:284-316
-    template <bool WJ, bool FAST = false>
+    template <bool WJ, bool FAST = false, bool EXACT = false>
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], wf = c.p[4];
         T r2 = x * x + y * y;
         T r = sqrt(r2);
         const T tan_w_half = c.p[8];  // tan(w / 2), host-precomputed (acm.hip prep)
-        T atan_wrd = atan2_ge0(T(2) * tan_w_half * r, z);  // y >= 0
+        T atan_wrd = EXACT ? atan2_exact(T(2) * tan_w_half * r, z)  // y >= 0
+                           : atan2_ge0(T(2) * tan_w_half * r, z);
         const bool axis = r2 < T(kEpsSqrt);
         const T irw = FAST ? T(1) / (r * wf) : T(0);
         T rd = axis ? T(2) * tan_w_half / wf : (FAST ? atan_wrd * irw : atan_wrd / (r * wf));

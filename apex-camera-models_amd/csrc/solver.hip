@@ -335,11 +335,21 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
     std::vector<double> h(R);
     // Without an all-reduce the epilogue kernel writes the R results straight
     // into pinned, device-mapped host memory: no device-to-host copy launch
-    // per evaluation (one buffer per host thread, kept for the process).  In
-    // mode 2 it also publishes a sequence number in the buffer's last word,
-    // and the host spins on that word instead of synchronising the stream.
-    static thread_local double* pinned = nullptr;
-    static thread_local unsigned long long seq = 0;
+    // per evaluation.  One buffer per host thread (calls on different threads
+    // never share it), owned by a thread_local that frees it when the thread
+    // exits.  In mode 2 the kernel also publishes a sequence number in the
+    // buffer's last word, and the host spins on that word instead of
+    // synchronising the stream.
+    struct PinnedResults {
+        double* p = nullptr;
+        unsigned long long seq = 0;
+        ~PinnedResults() {
+            if (p && hipHostFree(p) != hipSuccess) (void)hipGetLastError();
+        }
+    };
+    static thread_local PinnedResults tl;
+    double*& pinned = tl.p;
+    unsigned long long& seq = tl.seq;
     const int host_mode = allreduce ? 0 : acm::lm_host_result();
     double* res_out = d_res;
     unsigned long long* flag = nullptr;

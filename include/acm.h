@@ -94,6 +94,15 @@ typedef enum acm_validation {
 
 enum { ACM_LAYOUT_AOS = 0, ACM_LAYOUT_SOA = 1 };
 
+/* Per-call option OR-ed into acm_project's `layout`: reference-exact math for
+ * Kannala-Brandt and FOV (IEEE sqrt / divisions and a correctly rounded
+ * double-double atan2 instead of the fast polynomial / rsq forms, ~1e-16
+ * apart).  Projections and Jacobians then equal the reference (Rust f64 +
+ * glibc libm) bit for bit wherever glibc's atan2 is correctly rounded, i.e.
+ * on all but ~0.2% of arguments, where the two differ by one ulp.  The other
+ * five models are reference-exact without it (the flag is ignored). */
+enum { ACM_EXACT_MATH = 0x100 };
+
 /* Invalid-point policy of the factor evaluation (apex-solver source absent:
  * "skip" matches compute_reprojection_error skipping failed projections,
  * error_metrics.rs:76; "sentinel" is the (1e6,1e6) residual of the removed
@@ -129,7 +138,8 @@ ACM_API int acm_camera_init(acm_camera *cam, int model, const double *params,
 ACM_API int acm_validate_params(const acm_camera *cam);
 
 /* Batched CameraModel::project (+ optional dense parameter Jacobian).
- * points_3d: 3N f64 (layout), points_2d: 2N f64 out, status: N u8 out,
+ * points_3d: 3N f64 (layout, optionally | ACM_EXACT_MATH), points_2d: 2N f64
+ * out, status: N u8 out,
  * jacobian: 2N*P f64 out or NULL.  Failed points: uv = NaN, J = 0.
  * Replaces mod.rs:256 (per point) and the factor's Jacobian. */
 ACM_API int acm_project(const acm_camera *cam, size_t n,
@@ -388,6 +398,11 @@ ACM_API int acm_stream_synchronize(void *stream);
  * divide by fx, fy through the host's correctly rounded 1/fx, 1/fy and one
  * FMA correction, bit-identical to the division (-1 = auto = on, 0 = plain
  * IEEE divisions, 1 = on).
+ * ACM_TUNE_SAMPLE_PATIENCE: polls the single-pass sample_points look-back
+ * spends on a predecessor tile that has not published its count before the
+ * waiting wave counts that tile's cells itself (-1 = auto = 512; 0 = at once,
+ * which exercises that path; outputs are identical for every value).
+ * Every knob is an atomic: acm_set_tuning may race with any other call.
  * Returns the previous value or an error. */
 enum {
     ACM_TUNE_PROJECT_VARIANT = 0,
@@ -400,7 +415,8 @@ enum {
     ACM_TUNE_NT_LOADS_UNPROJECT = 7,
     ACM_TUNE_LM_HOST_RESULT = 8,
     ACM_TUNE_SAMPLE_FUSED = 9,
-    ACM_TUNE_UNPROJECT_RCP = 10
+    ACM_TUNE_UNPROJECT_RCP = 10,
+    ACM_TUNE_SAMPLE_PATIENCE = 11
 };
 ACM_API int acm_set_tuning(int key, int value);
 

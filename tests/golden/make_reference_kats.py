@@ -23,6 +23,7 @@ UCM_SAMPLE = [1313.83, 1313.27, 960.471, 546.981, 1.01674]
 EUCM_SAMPLE = [1313.83, 1313.27, 960.471, 546.981, 1.01674, 0.5]
 RADTAN_YAML = [461.629, 460.152, 362.680, 246.049, -0.28340811, 0.07395907, 0.00019359,
                1.76187114e-05, 0.0]
+FOV_YAML = [379.045, 379.008, 505.512, 509.969, 0.9259487501905697]  # fov.rs:508-522, samples/fov.yaml
 FIVE_POINTS = [[0.1, 0.1, 1.0], [0.3, 0.0, 1.5], [-0.2, 0.3, 2.0], [-0.3, -0.2, 1.8],
                [0.15, -0.25, 2.5]]  # tests/model_conversions.rs:9-17
 
@@ -52,6 +53,16 @@ KATS = {
          "status": "PointIsOutSideImage", "src": "src/camera/eucm.rs:634-662"},
         {"model": "eucm", "params": EUCM_SAMPLE, "res": [752, 480], "point": [0.1, 0.2, -1.0],
          "status": "PointIsOutSideImage", "src": "src/camera/eucm.rs:665-672"},
+        {"model": "fov", "params": FOV_YAML, "res": [752, 480], "point": [0.0, 0.0, 0.0],
+         "status": "PointAtCameraCenter", "src": "src/camera/fov.rs:647-655"},
+        {"model": "fov", "params": FOV_YAML, "res": [752, 480], "point": [0.1, 0.2, -1.0],
+         "status": "PointAtCameraCenter", "src": "src/camera/fov.rs:658-666"},
+    ],
+    # `if let Ok(p) = model.project(..)`: any error is accepted, an Ok result
+    # must land within tol of the principal point
+    "project_near_center_if_ok": [
+        {"model": "fov", "params": FOV_YAML, "res": [752, 480], "point": [0.0, 0.0, 0.1],
+         "tol": 1e-3, "src": "src/camera/fov.rs:638-645"},
     ],
     # DS/UCM/EUCM near-origin point: either PointIsOutSideImage or ~(cx, cy) +-1e-3
     "project_near_center": [
@@ -90,6 +101,10 @@ KATS = {
          "tol": 1e-4, "in_bounds": False, "src": "src/camera/eucm.rs:576-605"},
         {"model": "eucm", "params": EUCM_SAMPLE, "res": [752, 480], "point": [0.0, 0.0, 1.0],
          "tol": 1e-6, "in_bounds": False, "center_tol": 1.0, "src": "src/camera/eucm.rs:608-630"},
+        {"model": "fov", "params": FOV_YAML, "res": [752, 480], "point": [0.1, 0.1, 3.0],
+         "tol": 1e-4, "in_bounds": False, "finite": True, "src": "src/camera/fov.rs:576-606"},
+        {"model": "fov", "params": FOV_YAML, "res": [752, 480], "point": [0.0, 0.0, 1.0],
+         "tol": 1e-6, "in_bounds": False, "center_tol": 1.0, "src": "src/camera/fov.rs:609-631"},
     ],
     # dot(normalize(p), unproject(project(p))) >= min_dot for successful projections
     "round_trip_dot": [
@@ -114,11 +129,19 @@ KATS = {
          "error": "PrincipalPointMustBeFinite", "src": "tests/model_conversions.rs:181-182"},
         {"model": "pinhole", "params": [500.0, 500.0, 320.0, "nan"],
          "error": "PrincipalPointMustBeFinite", "src": "tests/model_conversions.rs:184-185"},
+        {"model": "fov", "params": FOV_YAML, "error": "Valid", "src": "src/camera/fov.rs:668-673"},
+    ] + [
+        {"model": "fov", "params": FOV_YAML[:4] + [w], "error": "InvalidParams",
+         "src": "src/camera/fov.rs:677-703"} for w in (0.0, -0.5, 3.5, "nan")
+    ] + [
+        {"model": "fov", "params": [0.0] + FOV_YAML[1:], "error": "FocalLengthMustBePositive",
+         "src": "src/camera/fov.rs:705-714"},
     ],
     "param_count_errors": [
         {"model": "double_sphere", "n": 2}, {"model": "kannala_brandt", "n": 1},
         {"model": "rad_tan", "n": 2}, {"model": "ucm", "n": 1}, {"model": "eucm", "n": 1},
         {"model": "pinhole", "n": 1},
+        {"model": "fov", "n": 4, "src": "src/camera/fov.rs:750-756"},
     ],
     "param_count_errors_src": "tests/model_conversions.rs:162-169",
     "yaml_values": {
@@ -127,6 +150,7 @@ KATS = {
         "double_sphere": {"params": DS_YAML, "res": [752, 480],
                           "src": "src/camera/double_sphere.rs:677-692"},
         "rad_tan": {"params": RADTAN_YAML, "res": [752, 480], "src": "src/camera/rad_tan.rs:806-825"},
+        "fov": {"params": FOV_YAML, "res": [752, 480], "src": "src/camera/fov.rs:524-537"},
     },
     "sample_points": {"model": "double_sphere", "params": DS_YAML, "res": [752, 480], "n": 100,
                       "src": "src/util/mod.rs:70-95"},

@@ -37,6 +37,14 @@ def run_project_near_center(be):
             assert st[0] == STATUS["PointIsOutSideImage"], k["src"]
 
 
+def run_project_near_center_if_ok(be):
+    for k in KATS["project_near_center_if_ok"]:
+        p = parse_params(k["params"])
+        uv, st, _ = be.project(MODEL_IDS[k["model"]], p, *k["res"], [k["point"]], want_jac=False)
+        if st[0] == 0:
+            assert abs(uv[0, 0] - p[2]) < k["tol"] and abs(uv[0, 1] - p[3]) < k["tol"], k["src"]
+
+
 def run_unproject_status(be):
     for k in KATS["unproject_status"]:
         _, st = be.unproject(MODEL_IDS[k["model"]], parse_params(k["params"]), *k["res"],
@@ -50,6 +58,8 @@ def run_round_trip(be):
         pt = np.array(k["point"])
         uv, st, _ = be.project(m, p, w, h, [pt], want_jac=False)
         assert st[0] == 0, k["src"]
+        if k.get("finite"):
+            assert np.isfinite(uv[0]).all(), k["src"]
         if k.get("in_bounds"):
             assert 0 <= uv[0, 0] < w and 0 <= uv[0, 1] < h, k["src"]
         if "center_tol" in k:
@@ -78,5 +88,5 @@ def run_round_trip_dot(be):
         assert np.all(dots > k["min_dot"]), (k["src"], dots)
 
 
-ALL = [run_project_value, run_project_status, run_project_near_center, run_unproject_status,
-       run_round_trip, run_round_trip_dot]
+ALL = [run_project_value, run_project_status, run_project_near_center,
+       run_project_near_center_if_ok, run_unproject_status, run_round_trip, run_round_trip_dot]

@@ -46,7 +46,11 @@ def _init(model, params, w=752, h=480):
 def test_camera_init_param_count_errors():
     # tests/model_conversions.rs:162-169: wrong parameter counts -> InvalidParams
     from apex_camera_models import _lib
-    for model, n in [(3, 2), (2, 1), (1, 2), (4, 1), (5, 1), (0, 1)]:
+    import kat_suite
+    from _backends import MODEL_IDS
+    cases = [(MODEL_IDS[k["model"]], k["n"]) for k in kat_suite.KATS["param_count_errors"]]
+    assert (6, 4) in cases  # fov.rs:750-756
+    for model, n in cases:
         rc, _ = _init(model, [500.0] * n)
         assert rc == _lib.ERR_INVALID_PARAMS
     assert "Expected" in _lib.last_error()
@@ -61,6 +65,28 @@ def test_camera_init_validates_pinhole_like_reference():
               [500.0, 500.0, math.inf, 240.0], [500.0, 500.0, 320.0, math.nan]):
         rc, _ = _init(0, p)
         assert rc == _lib.ERR_INVALID_PARAMS
+
+
+def test_validate_params_reference_kats():
+    """tests/golden/reference_kats.json "validate_params" (pinhole: the
+    reference runs it inside new(); FOV: fov.rs:668-714) through the C-ABI's
+    acm_validate_params, whose codes mirror CameraModelError (acm.h)."""
+    import kat_suite
+    from _backends import MODEL_IDS, parse_params
+    from apex_camera_models import _lib
+    L = _lib.load()
+    code = {"Valid": 0, "FocalLengthMustBePositive": 4, "PrincipalPointMustBeFinite": 5,
+            "InvalidParams": 6}
+    n_fov = 0
+    for k in kat_suite.KATS["validate_params"]:
+        p = parse_params(k["params"])
+        cam = _lib.AcmCamera()
+        cam.model, cam.width, cam.height, cam.num_params = MODEL_IDS[k["model"]], 752, 480, len(p)
+        for i, v in enumerate(p):
+            cam.params[i] = v
+        assert L.acm_validate_params(ctypes.byref(cam)) == code[k["error"]], k["src"]
+        n_fov += k["model"] == "fov"
+    assert n_fov == 6
 
 
 def test_validate_params_codes():

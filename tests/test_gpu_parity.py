@@ -309,6 +309,36 @@ def test_sample_points_every_path_matches_oracle(model):
         L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, -1)
 
 
+@pytest.mark.parametrize("model", [1, 2, 4])
+def test_sample_points_lookback_fallback(model):
+    """ACM_TUNE_SAMPLE_PATIENCE = 0: a tile whose predecessor has not yet
+    published its count counts that predecessor's cells itself at once (the
+    path that guarantees progress whatever the dispatch order).  Outputs stay
+    bit-identical to the default run and the oracle."""
+    from apex_camera_models import _lib, util
+    from test_oracle import SAMPLES
+    params, (w, h) = SAMPLES[model]
+    m = _model_obj(model, params, w, h)
+    n = 2_000_000
+    L = _lib.load()
+    uv_d, xyz_d = util.sample_points(m, n)
+    try:
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_PATIENCE, 0)
+        for _ in range(3):
+            uv, xyz = util.sample_points(m, n)
+            assert torch_equal_bits(uv, uv_d) and torch_equal_bits(xyz, xyz_d)
+    finally:
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_PATIENCE, -1)
+    uv0, xyz0, _ = O.sample_points(model, params, w, h, n)
+    assert np.array_equal(uv.cpu().numpy(), uv0)
+
+
+def torch_equal_bits(a, b):
+    import torch
+    return a.shape == b.shape and torch.equal(a.contiguous().view(torch.int64),
+                                              b.contiguous().view(torch.int64))
+
+
 def test_full_size_kb_properties():
     """BASELINE config 2 size (10M): properties that need no oracle run over the
     whole batch, plus an oracle check of a 200k-point strided subsample."""

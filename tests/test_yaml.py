@@ -123,3 +123,29 @@ def test_model_names_and_getters():  # mod.rs:583-620, kannala_brandt.rs:976-997
     assert acm.UcmModel.new([350.0, 350.0, 320.0, 240.0, 0.8]).get_model_name() == "ucm"
     ds = acm.DoubleSphereModel.new([350.0, 350.0, 320.0, 240.0, 0.58, -0.18])
     assert ds.get_distortion() == [0.58, -0.18]  # [alpha, xi] (double_sphere.rs:636-638)
+
+
+def test_fov_reference_kats():
+    """fov.rs:524-537 (samples/fov.yaml values), :668-714 (validate_params),
+    :750-756 (parameter count) -- tests/golden/reference_kats.json."""
+    import apex_camera_models as acm
+    import kat_suite
+    from _backends import parse_params
+    from apex_camera_models.camera import FocalLengthMustBePositive, InvalidParams
+    y = kat_suite.KATS["yaml_values"]["fov"]
+    m = acm.FovModel.load_from_yaml(path("fov.yaml"))
+    assert m.params() == y["params"]
+    assert (m.resolution.width, m.resolution.height) == tuple(y["res"])
+    errs = {"Valid": None, "InvalidParams": InvalidParams,
+            "FocalLengthMustBePositive": FocalLengthMustBePositive}
+    for k in kat_suite.KATS["validate_params"]:
+        if k["model"] != "fov":
+            continue
+        mm = acm.FovModel.new(parse_params(k["params"]))
+        if errs[k["error"]] is None:
+            mm.validate_params()
+        else:
+            with pytest.raises(errs[k["error"]]):
+                mm.validate_params()
+    with pytest.raises(InvalidParams):
+        acm.FovModel.new([379.045, 379.008, 505.512, 509.969])

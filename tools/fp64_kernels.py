@@ -1,0 +1,110 @@
+"""Driver for the counter passes of the kernels DESIGN.md calls FP64-VALU
+bound: RadTan and KB unproject (10M pixels), KB fused
+normal equations (10M points), the FOV grid search (9.3M KB-sampled
+correspondences) and the fused sample_points (1e8-cell KB grid).  Each runs
+`--reps` times after one warm-up; the HIP-event time per call is printed as
+one JSON line per kernel, so the same command under `rocprofv3 --pmc ...`
+yields per-dispatch counters and the event times side by side.
+
+  python tools/fp64_kernels.py [--only radtan_unproject,kb_unproject,...] [--reps 5]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "apex-camera-models_amd"))
+sys.path.insert(0, ROOT)
+
+ALL = ("radtan_unproject", "kb_unproject", "kb_normal_eq", "fov_grid", "sample_kb")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=",".join(ALL))
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--points", type=int, default=10_000_000)
+    ap.add_argument("--cells", type=int, default=100_000_000)
+    ap.add_argument("--sample-fused", type=int, default=None,
+                    help="ACM_TUNE_SAMPLE_FUSED for sample_kb (-1 auto, 0 two-pass, 1/2/3 = R 4/8/16)")
+    ap.add_argument("--lib", default=None, help="load this libacm build instead (diagnostic "
+                    "builds: make -C apex-camera-models_amd diag)")
+    a = ap.parse_args()
+    want = set(a.only.split(","))
+    if a.lib:
+        os.environ["ACM_LIB_PATH"] = os.path.abspath(a.lib)
+    import torch
+    from apex_camera_models import KannalaBrandtModel, Resolution, _lib, conversion, factors
+    from apex_camera_models import samples, util
+    L = _lib.load()
+    assert os.path.samefile(_lib.LIB_PATH, a.lib or _lib.LIB_PATH)
+    sh = torch.cuda.current_stream().cuda_stream
+    n = a.points
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / a.reps
+
+    def emit(name, units, ms, bytes_per_unit, **kw):
+        d = {"kernel": name, "units": units, "ms": round(ms, 4),
+             "GBps": round(bytes_per_unit * units / ms / 1e6, 1) if bytes_per_unit else None, **kw}
+        print(json.dumps(d), flush=True)
+
+    pts = samples.synthetic_points_device(n)
+    for mid, name in ((1, "radtan_unproject"), (2, "kb_unproject")):
+        if name not in want:
+            continue
+        params, (w, h) = samples.SAMPLES[mid]
+        cam = _lib.AcmCamera()
+        _lib.check(L.acm_camera_init(ctypes.byref(cam), mid, (ctypes.c_double * len(params))(
+            *params), len(params), w, h))
+        uv = torch.empty((n, 2), dtype=torch.float64, device="cuda")
+        st = torch.empty((n,), dtype=torch.uint8, device="cuda")
+        L.acm_project(ctypes.byref(cam), n, pts.data_ptr(), 0, uv.data_ptr(), st.data_ptr(),
+                      None, sh)
+        uv = torch.nan_to_num(uv, nan=1.0).contiguous()
+        rays = torch.empty((n, 3), dtype=torch.float64, device="cuda")
+        ms = timed(lambda: L.acm_unproject(ctypes.byref(cam), n, uv.data_ptr(), rays.data_ptr(),
+                                           0, st.data_ptr(), sh))
+        emit(name, n, ms, 41)
+        del uv, rays, st
+    if "kb_normal_eq" in want:
+        p2 = pts[torch.isfinite(pts).all(1)].contiguous()
+        params, (w, h) = samples.SAMPLES[2]
+        m = KannalaBrandtModel._from_params(list(params), Resolution(w, h))
+        uv, _, _ = m.project_batch(p2)
+        obs = torch.nan_to_num(uv, nan=0.0) + 0.25
+        f = factors.KannalaBrandtCameraParamsFactor(p2, obs, Resolution(w, h))
+        out = torch.empty((8 * 8 + 8 + 2,), dtype=torch.float64, device="cuda")
+        ms = timed(lambda: f.normal_equations(params, out))
+        emit("kb_normal_eq", p2.shape[0], ms, 40)
+        del p2, uv, obs, f
+    del pts
+    kp, (kw, kh) = samples.SAMPLES[2]
+    src = KannalaBrandtModel._from_params(kp, Resolution(kw, kh))
+    if "fov_grid" in want:
+        suv, sxyz = util.sample_points(src, n)
+        fov = conversion._init_target("fov", src)
+        ms = timed(lambda: fov.linear_estimation(sxyz, suv))
+        emit("fov_grid", sxyz.shape[0], ms, 40, evaluations=290 * sxyz.shape[0])
+        del suv, sxyz
+    if "sample_kb" in want:
+        if a.sample_fused is not None:
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, a.sample_fused)
+        kept = util.sample_points(src, a.cells)[0].shape[0]
+        ms = timed(lambda: util.sample_points(src, a.cells))
+        emit("sample_kb", a.cells, ms, None, kept=kept,
+             kept_GBps=round(40 * kept / ms / 1e6, 1))
+
+
+if __name__ == "__main__":
+    main()
