@@ -98,6 +98,7 @@ EXPORTED_SYMBOLS = (
     "acm_normal_equations",
     "acm_reprojection_stats_workspace_size",
     "acm_reprojection_stats",
+    "acm_reprojection_stats_merge",
     "acm_linear_system_columns",
     "acm_linear_system_qr_workspace_size",
     "acm_linear_system_qr",
@@ -175,6 +176,9 @@ def load():
     L.acm_normal_equations.restype = i
     L.acm_reprojection_stats_workspace_size.argtypes = [sz]
     L.acm_reprojection_stats_workspace_size.restype = sz
+    L.acm_reprojection_stats_merge.argtypes = [sz, ctypes.POINTER(ctypes.c_double),
+                                               ctypes.POINTER(ctypes.c_double)]
+    L.acm_reprojection_stats_merge.restype = i
     L.acm_reprojection_stats.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp, sz, vp]
     L.acm_reprojection_stats.restype = i
     L.acm_sample_points_grid.argtypes = [ctypes.c_uint32, ctypes.c_uint32, sz,

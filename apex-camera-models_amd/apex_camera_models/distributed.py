@@ -74,32 +74,62 @@ def allreduce_normal_equations(vec: torch.Tensor, group=None) -> torch.Tensor:
 
 
 # --------------------------------------------------- reprojection statistics
+STAT_KEYS = ("rmse", "min", "max", "mean", "stddev", "n_valid", "sum", "sumsq")
+
+
+def local_reprojection_result(errors) -> torch.Tensor:
+    """acm_reprojection_stats' 8-double result [rmse, min, max, mean, stddev,
+    n_valid, sum, sumsq] of one shard's per-point errors computed on the
+    host (NaN = invalid) -- for shards whose errors come from elsewhere, e.g.
+    the CPU oracle in the gloo tests."""
+    import numpy as np
+    e = np.asarray(errors.cpu() if isinstance(errors, torch.Tensor) else errors,
+                   dtype=np.float64)
+    v = e[~np.isnan(e)]
+    n = float(v.size)
+    if n == 0:
+        return torch.tensor([np.nan, np.inf, -np.inf, np.nan, np.nan, 0.0, 0.0, 0.0],
+                            dtype=torch.float64)
+    s, ss = float(v.sum()), float((v * v).sum())
+    mean = s / n
+    return torch.tensor([(ss / n) ** 0.5, float(v.min()), float(v.max()), mean,
+                         (float(((v - mean) ** 2).sum()) / n) ** 0.5, n, s, ss],
+                        dtype=torch.float64)
+
+
+def merge_reprojection_stats(local_result: torch.Tensor, group=None) -> dict:
+    """error_metrics.rs:86-111 over the union of every rank's shard: ONE
+    all-gather of each rank's 8-double acm_reprojection_stats result, then
+    libacm's rank-ordered merge (acm_reprojection_stats_merge: sums, extrema,
+    Chan's update of (n, mean, M2)) -- every rank computes the same numbers
+    bit for bit.  No mask copy, no per-statistic all-reduce, no second
+    variance pass over the errors."""
+    import ctypes
+
+    from . import _lib
+    world = dist.get_world_size(group)
+    be = dist.get_backend(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if be == "nccl" else \
+        torch.device("cpu")
+    mine = local_result.reshape(8).to(dev, torch.float64).contiguous()
+    allr = [torch.empty((8,), dtype=torch.float64, device=dev) for _ in range(world)]
+    dist.all_gather(allr, mine, group=group)
+    parts = torch.stack(allr).cpu().contiguous()
+    out = (ctypes.c_double * 8)()
+    _lib.check(_lib.load().acm_reprojection_stats_merge(
+        world, ctypes.cast(parts.data_ptr(), ctypes.POINTER(ctypes.c_double)), out))
+    d = dict(zip(STAT_KEYS, list(out)))
+    d["n_valid"] = int(d["n_valid"])
+    return d
+
+
 def combine_reprojection_stats(local_errors: torch.Tensor, group=None) -> dict:
-    """error_metrics.rs:86-111 over the union of all ranks' valid errors
-    (local_errors: this rank's per-point errors, NaN = failed projection).
-    Sums / min / max are all-reduced; the median of the union comes from
-    libacm's radix select with its per-pass histograms all-reduced
-    (distributed_median) when the errors live on the GPU."""
-    valid = local_errors[~torch.isnan(local_errors)]
-    dev = local_errors.device
-    s = torch.stack([valid.sum(), (valid * valid).sum(),
-                     torch.tensor(float(valid.numel()), dtype=torch.float64, device=dev)])
-    mn = valid.min() if valid.numel() else torch.tensor(float("inf"), dtype=torch.float64,
-                                                         device=dev)
-    mx = valid.max() if valid.numel() else torch.tensor(float("-inf"), dtype=torch.float64,
-                                                         device=dev)
-    mn, mx = mn.clone().reshape(1), mx.clone().reshape(1)
-    dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
-    dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
-    n = float(s[2])
-    mean = float(s[0]) / n
-    var = ((valid - mean) ** 2).sum().reshape(1)
-    dist.all_reduce(var, op=dist.ReduceOp.SUM, group=group)
-    out = {"rmse": (float(s[1]) / n) ** 0.5, "min": float(mn), "max": float(mx), "mean": mean,
-           "stddev": (float(var) / n) ** 0.5, "n_valid": int(n)}
-    if local_errors.is_cuda:
-        out["median"] = distributed_median(local_errors, int(n), group)
+    """Statistics of the union of every rank's per-point errors (NaN =
+    invalid) via merge_reprojection_stats; for GPU errors also the exact
+    median of the union (distributed_median)."""
+    out = merge_reprojection_stats(local_reprojection_result(local_errors), group)
+    if local_errors.is_cuda and out["n_valid"] > 0:
+        out["median"] = distributed_median(local_errors, out["n_valid"], group)
     return out
 
 
@@ -187,10 +217,11 @@ def distributed_reprojection_error(model, points_3d, points_2d, group=None):
     from .camera import _as_device_f64
     p3 = _as_device_f64(points_3d, 3)
     errors = torch.empty((p3.shape[0],), dtype=torch.float64, device=p3.device)
-    util.reprojection_stats(model, p3, points_2d, errors)
-    st = combine_reprojection_stats(errors, group)
-    if st["n_valid"] == 0:
+    local = util.reprojection_stats(model, p3, points_2d, errors)  # this shard, on the GPU
+    st = merge_reprojection_stats(local, group)
+    if st["n_valid"] == 0:  # error_metrics.rs:82-84, on every rank alike
         raise util.ZeroProjectionPoints()
+    st["median"] = distributed_median(errors, st["n_valid"], group)
     return util.ProjectionError(rmse=st["rmse"], min=st["min"], max=st["max"], mean=st["mean"],
                                 stddev=st["stddev"], median=st["median"], n_valid=st["n_valid"])
 

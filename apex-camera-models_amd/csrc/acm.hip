@@ -1004,6 +1004,13 @@ __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t 
             if (st == ST_OK) {
                 const double du = u - o[k].x, dv = v - o[k].y;
                 e = sqrt(du * du + dv * dv);
+            }
+            // One validity rule for the statistics and the median: an Ok
+            // projection whose error is NaN (a NaN observation) is not a
+            // valid error -- acm_median_valid skips NaN too.  (The reference
+            // would sum the NaN and then panic in its median sort,
+            // error_metrics.rs:104-108 partial_cmp().unwrap().)
+            if (e == e) {
                 s += e;
                 ss += e * e;
                 mn = fmin(mn, e);
@@ -2492,6 +2499,41 @@ ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double
         hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, result);
         return check_launch("acm_reprojection_stats");
     });
+}
+
+ACM_API int acm_reprojection_stats_merge(size_t nparts, const double* parts, double* result) {
+    if (!result || (nparts && !parts)) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL argument");
+    // parts: nparts x [rmse, min, max, mean, stddev, n_valid, sum, sumsq]
+    // (acm_reprojection_stats results of disjoint shards), merged in order:
+    // sums add, extrema combine, (n, mean, M2 = n stddev^2) by Chan's update
+    double n = 0.0, sum = 0.0, sumsq = 0.0, mn = INFINITY, mx = -INFINITY, m = 0.0, M2 = 0.0;
+    for (size_t r = 0; r < nparts; ++r) {
+        const double* p = parts + 8 * r;
+        const double nr = p[5];
+        if (!(nr > 0.0)) continue;
+        sum += p[6];
+        sumsq += p[7];
+        mn = std::fmin(mn, p[1]);
+        mx = std::fmax(mx, p[2]);
+        const double mr = p[3], M2r = p[4] * p[4] * nr;
+        if (n == 0.0) {
+            n = nr; m = mr; M2 = M2r;
+        } else {
+            const double t = n + nr, d = mr - m;
+            m = m + d * (nr / t);
+            M2 = M2 + M2r + d * d * (n * (nr / t));
+            n = t;
+        }
+    }
+    result[0] = std::sqrt(sumsq / n);
+    result[1] = mn;
+    result[2] = mx;
+    result[3] = sum / n;  // error_metrics.rs:88-89: sum / n
+    result[4] = std::sqrt(std::fmax(M2, 0.0) / n);
+    result[5] = n;
+    result[6] = sum;
+    result[7] = sumsq;
+    return ACM_SUCCESS;
 }
 
 ACM_API int acm_sample_points_grid(uint32_t width, uint32_t height, size_t n_requested,

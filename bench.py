@@ -1,18 +1,24 @@
 """Benchmark of the hot path: Kannala-Brandt project + dense 2x8 parameter
-Jacobian over 10M f64 points per GPU (BASELINE.json configs[1], the config
-the metric is quoted on).
+Jacobian, 10M f64 points (BASELINE.json configs[1], the config the metric
+is quoted on).
 
 One step = one pass of acm_project (the C-ABI of libacm.so) over the resident
-10M-point batch: reads xyz (24 B/pt), writes uv (16 B), status (1 B) and the
-2N x 8 column-major Jacobian (128 B) = 169 B/pt algorithmic traffic.
+batch: reads xyz (24 B/pt), writes uv (16 B), status (1 B) and the 2N x 8
+column-major Jacobian (128 B) = 169 B/pt algorithmic traffic.
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W] [--scaling weak|strong]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Multi-GPU: one process per GPU, each rank projects its own 10M-point shard
-(weak scaling, disjoint seeded shards, no data-path collective -- the path is
-a pure per-point map); timing is barrier + synchronize on both sides and the
-max over ranks.  rank 0 prints ONE JSON line.
+Multi-GPU: one process per GPU.  --scaling weak (default): each rank
+projects its own --points batch (disjoint seeded shards; total work grows
+with N).  --scaling strong: --points is the GLOBAL batch, split into
+contiguous shards (distributed.shard_range: 10M -> 1.25M per rank at 8 GPUs).
+The path is a pure per-point map, so the timed steps have no data-path
+collective; at N > 1 the line also carries the other scaling mode measured
+in the same run, and the north-star collective -- one RCCL all-reduce of
+(sum ||r||^2, n_valid) of a residual pass over each rank's shard -- timed on
+its own.  Timing is barrier + synchronize on both sides and the max over
+ranks; rank 0 prints ONE JSON line.
 """
 import argparse
 import ctypes
@@ -37,7 +43,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--points", type=int, default=10_000_000, help="points per GPU")
+    ap.add_argument("--points", type=int, default=10_000_000,
+                    help="points per GPU (weak) or in total (strong)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--verify-shards", action="store_true",
+                    help="(tests) strong mode: gather every rank's uv/status and compare "
+                         "with one projection of the global batch on rank 0")
     ap.add_argument("--model", default="kb", choices=sorted(MODELS))
     ap.add_argument("--layout", default="aos", choices=["aos", "soa"])
     ap.add_argument("--no-jacobian", action="store_true")
@@ -46,10 +57,12 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(model_id, params, w, h, n, seconds):
+def cpu_baseline(model_id, params, w, h, n, seconds, opt="O3"):
     """Oracle (C restatement of the reference's single-threaded per-point
     Rust loop) timed on this host, 1 thread, on the same 10M-point workload,
-    repeated until `seconds` of CPU work; median throughput."""
+    repeated until `seconds` of CPU work; median throughput.  opt: the
+    -O3 -ffp-contract=off build (the planned
+    baseline) or the -O2 parity build."""
     import numpy as np
 
     import oracle
@@ -59,7 +72,7 @@ def cpu_baseline(model_id, params, w, h, n, seconds):
     uv = np.empty((n, 2))
     st = np.empty(n, dtype=np.uint8)
     jac = np.empty((P, n, 2))
-    L = oracle.lib()
+    L = oracle.lib(opt)
     dp = oracle._dp
     pa = np.ascontiguousarray(params, dtype=np.float64)
     rates, t_total = [], 0.0
@@ -75,7 +88,7 @@ def cpu_baseline(model_id, params, w, h, n, seconds):
     rates.sort()
     return {"value": rates[len(rates) // 2], "unit": "Mpoints/s", "cores": 1, "kind": "port",
             "sample": f"{len(rates)} x full {n}-point batch (project + 2x{P} J), "
-                      f"{t_total:.1f} s of CPU work, median; oracle/acm_oracle.c -O2 "
+                      f"{t_total:.1f} s of CPU work, median; oracle/acm_oracle.c -{opt} "
                       f"-ffp-contract=off, 1 thread"}
 
 
@@ -102,7 +115,7 @@ def cpu_baseline_all_cores(model_id, params, w, h, n, seconds, threads):
     from apex_camera_models import samples
     pts = samples.synthetic_points(n)
     P = oracle.NUM_PARAMS[model_id]
-    L = oracle.lib()
+    L = oracle.lib("O3")
     dp = oracle._dp
     pa = np.ascontiguousarray(params, dtype=np.float64)
     bounds = [(n * t // threads, n * (t + 1) // threads) for t in range(threads)]
@@ -134,13 +147,24 @@ def cpu_baseline_all_cores(model_id, params, w, h, n, seconds, threads):
     return {"value": rates[len(rates) // 2], "unit": "Mpoints/s", "cores": threads,
             "kind": "port",
             "sample": f"{len(rates)} x full {n}-point batch (project + 2x{P} J) split over "
-                      f"{threads} threads, {t_total:.1f} s wall, median; same oracle build"}
+                      f"{threads} threads, {t_total:.1f} s wall, median; -O3 oracle build"}
+
+
+def lib_sha256():
+    import hashlib
+    from apex_camera_models import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()
 
 
 def load_traffic(workload, n):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
-    exact workload (profiles/*pmc*.json, written by profiles/collect_pmc.py),
-    else None."""
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary
+    of this exact workload (profiles/*pmc*.json, profiles/collect_pmc.py),
+    used only if it was collected on this very libacm.so (its sha256 is
+    recorded in the summary); otherwise traffic is null and the source says
+    why.  Returns (bytes or None, source description)."""
     import glob
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
@@ -149,8 +173,14 @@ def load_traffic(workload, n):
         except Exception:
             continue
         if d.get("workload") == workload and int(d.get("points", -1)) == n:
-            best = d
-    return best
+            best = (p, d)
+    if best is None:
+        return None, "no PMC summary for this workload"
+    p, d = best
+    rel = os.path.relpath(p, ROOT)
+    if d.get("libacm_sha256") != lib_sha256():
+        return None, f"{rel} was collected on another libacm.so build (stale): not reported"
+    return d["hbm_bytes_per_launch"], rel
 
 
 def main():
@@ -172,108 +202,229 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()
+        rank = dist.get_rank()
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # collectives' tensors
 
     from apex_camera_models import _lib, samples
+    from apex_camera_models.distributed import shard_range
     L = _lib.load()
     model_id = MODELS[a.model]
     params, (w, h) = samples.SAMPLES[model_id]
     P = len(params)
     want_j = not a.no_jacobian
-    n = a.points
     lay = _lib.LAYOUT_SOA if a.layout == "soa" else _lib.LAYOUT_AOS
 
     cam = _lib.AcmCamera()
     arr = (ctypes.c_double * P)(*params)
     _lib.check(L.acm_camera_init(ctypes.byref(cam), model_id, arr, P, w, h))
-
-    pts = samples.synthetic_points_device(n, offset=rank * n, layout=a.layout)
-    uv = torch.empty((n, 2), dtype=torch.float64, device=dev)
-    st = torch.empty((n,), dtype=torch.uint8, device=dev)
-    jac = torch.empty((P, n, 2), dtype=torch.float64, device=dev) if want_j else None
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
-    jp = jac.data_ptr() if want_j else None
 
-    def step():
-        rc = L.acm_project(ctypes.byref(cam), n, pts.data_ptr(), lay, uv.data_ptr(),
-                           st.data_ptr(), jp, sh)
-        if rc:
-            _lib.check(rc)
+    def points(mode):
+        """this rank's resident batch: (points tensor, n, global n)"""
+        if mode == "weak":
+            n = a.points
+            return samples.synthetic_points_device(n, offset=rank * n, layout=a.layout), n, \
+                n * world
+        lo, hi = shard_range(a.points, rank, world)
+        full = samples.synthetic_points_device(a.points, layout=a.layout)
+        if a.layout == "soa":
+            pts = full[:, lo:hi].contiguous()
+        else:
+            pts = full[lo:hi].contiguous()
+        del full
+        return pts, hi - lo, a.points
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
+    def measure(mode):
+        pts, n, n_global = points(mode)
+        uv = torch.empty((n, 2), dtype=torch.float64, device=dev)
+        st = torch.empty((n,), dtype=torch.uint8, device=dev)
+        jac = torch.empty((P, n, 2), dtype=torch.float64, device=dev) if want_j else None
+        jp = jac.data_ptr() if want_j else None
 
-    # One HIP event pair on the launch stream around the K back-to-back
-    # launches: the average launch duration includes the (sub-microsecond)
-    # gaps between launches, so `achieved` is conservative.  An event pair
-    # around every launch put ~5 us of extra gap between launches (wall
-    # 0.2499 vs 0.2433 ms per step, profiles/r01s8_diag_bench_gaps.log).
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        def step():
+            rc = L.acm_project(ctypes.byref(cam), n, pts.data_ptr(), lay, uv.data_ptr(),
+                               st.data_ptr(), jp, sh)
+            if rc:
+                _lib.check(rc)
+
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        # One HIP event pair on the launch stream around the K back-to-back
+        # launches: the average launch duration includes the (sub-microsecond)
+        # gaps between launches, so `achieved` is conservative.  An event pair
+        # around every launch put ~5 us of extra gap between launches (wall
+        # 0.2499 vs 0.2433 ms per step, profiles/r01s8_diag_bench_gaps.log).
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(a.steps):
+            step()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kern_ms = e0.elapsed_time(e1) / a.steps
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=cdev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+        ms_per_step = elapsed * 1e3 / a.steps
+        out = {"value": round(n_global / (ms_per_step / 1e3) / 1e6, 2),
+               "ms_per_step": round(ms_per_step, 5), "kernel_ms": round(kern_ms, 5),
+               "points_per_rank": n, "global_points": n_global}
+        if a.verify_shards and mode == "strong":
+            out["shards_match_single_projection"] = verify(pts, n, uv, st, jac)
+        return out, (pts, n)
+
+    def verify(pts, n, uv, st, jac):
+        """every rank's shard outputs, concatenated in rank order, equal one
+        projection of the whole global batch (bit for bit)"""
+        parts = [torch.cat([uv.reshape(-1), jac.reshape(-1) if jac is not None else
+                            uv.new_empty(0)]).cpu(), st.cpu()]
+        if world > 1:
+            gathered = [None] * world
+            dist.all_gather_object(gathered, parts)
+        else:
+            gathered = [parts]
+        if rank != 0:
+            return True
+        full = samples.synthetic_points_device(a.points, layout=a.layout)
+        N = a.points
+        uv1 = torch.empty((N, 2), dtype=torch.float64, device=dev)
+        st1 = torch.empty((N,), dtype=torch.uint8, device=dev)
+        j1 = torch.empty((P, N, 2), dtype=torch.float64, device=dev) if want_j else None
+        _lib.check(L.acm_project(ctypes.byref(cam), N, full.data_ptr(), lay, uv1.data_ptr(),
+                                 st1.data_ptr(), j1.data_ptr() if want_j else None, sh))
+        torch.cuda.synchronize()
+        uv_c = torch.cat([g[0][: 2 * len(g[1])].reshape(-1, 2) for g in gathered])
+        st_c = torch.cat([g[1] for g in gathered])
+        ok = torch.equal(st_c, st1.cpu()) and torch.equal(
+            uv_c.view(torch.int64), uv1.cpu().view(torch.int64))
+        if want_j:
+            jc = torch.cat([g[0][2 * len(g[1]):].reshape(P, -1, 2) for g in gathered], dim=1)
+            ok = ok and torch.equal(jc.view(torch.int64), j1.cpu().view(torch.int64))
+        return bool(ok)
+
+    main_res, (pts, n) = measure(a.scaling)
+    other = None
+    if world > 1:  # the other scaling mode, same process group, same run
+        del pts
+        other_mode = "strong" if a.scaling == "weak" else "weak"
+        other, _ = measure(other_mode)
+        other["mode"] = other_mode
+        pts, n, _ = points(a.scaling)  # the residual pass below runs on the primary shard
+
+    # The north-star collective: per rank one residual pass over its shard
+    # (acm_reprojection_stats against observations projected with fx * 1.01),
+    # then ONE all-reduce of (sum ||r||^2, n_valid) -- timed on its own.
+    pcam = _lib.AcmCamera()
+    pparams = list(params)
+    pparams[0] *= 1.01
+    _lib.check(L.acm_camera_init(ctypes.byref(pcam), model_id,
+                                 (ctypes.c_double * P)(*pparams), P, w, h))
+    obs = torch.empty((n, 2), dtype=torch.float64, device=dev)
+    sto = torch.empty((n,), dtype=torch.uint8, device=dev)
+    pts_aos = pts if a.layout == "aos" else pts.t().contiguous()
+    _lib.check(L.acm_project(ctypes.byref(pcam), n, pts_aos.data_ptr(), _lib.LAYOUT_AOS,
+                             obs.data_ptr(), sto.data_ptr(), None, sh))
+    res = torch.empty((8,), dtype=torch.float64, device=dev)
+    ws_b = L.acm_reprojection_stats_workspace_size(n)
+    ws = torch.empty(((ws_b + 7) // 8,), dtype=torch.float64, device=dev)
+    _lib.check(L.acm_reprojection_stats(ctypes.byref(cam), n, pts_aos.data_ptr(),
+                                        _lib.LAYOUT_AOS, obs.data_ptr(), res.data_ptr(), None,
+                                        ws.data_ptr(), ws_b, sh))
+    vec = torch.stack([res[7], res[5]]).to(cdev).contiguous()  # (sum ||r||^2, n_valid)
+    coll = {"op": "all_reduce(sum) of [sum ||r||^2, n_valid] (16 B)", "ranks": world}
     if world > 1:
+        red = vec.clone()
+        for _ in range(3):
+            red.copy_(vec)
+            dist.all_reduce(red)
+        torch.cuda.synchronize()
+        reps = 20
         dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(a.steps):
-        step()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = e0.elapsed_time(e1) / a.steps
-
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
-                     device=dev if backend == "nccl" else "cpu")
-    if world > 1:
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            red.copy_(vec)
+            dist.all_reduce(red)
+        torch.cuda.synchronize()
+        us = (time.perf_counter() - t0) / reps * 1e6
+        t = torch.tensor([us], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
-    ms_per_step = elapsed * 1e3 / a.steps
-    total_points = n * world
-    value = total_points / (ms_per_step / 1e3) / 1e6
+        coll["us"] = round(float(t[0]), 2)
+        coll["backend"] = dist.get_backend()
+    else:
+        red = vec
+        coll["us"] = None
+        coll["backend"] = None
+    red = red.cpu()
+    coll["global_sum_sq_px2"] = float(red[0])
+    coll["global_n_valid"] = int(red[1])
+    coll["global_rmse_px"] = (float(red[0]) / float(red[1])) ** 0.5 if float(red[1]) else None
 
     if rank == 0:
         bpp = 24 + 16 + 1 + (16 * P if want_j else 0)
-        achieved = bpp * n / (kern_ms / 1e3) / 1e9
+        kern_ms = main_res["kernel_ms"]
+        achieved = bpp * main_res["points_per_rank"] / (kern_ms / 1e3) / 1e9
         workload = (f"{a.model}_project{'_jacobian' if want_j else ''}_f64_"
                     f"{a.layout}")
-        pmc = load_traffic(workload, n)
-        traffic = pmc["hbm_bytes_per_launch"] if pmc else None
-        res = {
+        traffic, traffic_src = load_traffic(workload, main_res["points_per_rank"])
+        out = {
             "metric": "Mpoints/sec project+Jacobian (KB, f64) at 1/2/4/8 GPU; % HBM roofline",
-            "value": round(value, 2),
+            "value": main_res["value"],
             "unit": "Mpoints/s",
             "n_gpus": world,
+            "n_ranks_seen": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(ms_per_step, 5),
+            "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seed 20251205 Philox on device; x,y~U[-1,1), z~U[0.5,4), "
                     "0.1% edge points)",
-            "config": {"workload": workload, "points_per_gpu": n, "global_points": total_points,
+            "config": {"workload": workload, "points_per_gpu": main_res["points_per_rank"],
+                       "global_points": main_res["global_points"],
                        "model_params": "samples/kannala_brandt.yaml" if a.model == "kb"
                        else a.model, "jacobian_layout": "2N x P column-major (nalgebra DMatrix)",
-                       "parallelism": f"shard{world} (independent per-rank point batches)"},
+                       "parallelism": f"shard{world} ({a.scaling} scaling: "
+                                      + ("independent per-rank point batches)" if
+                                         a.scaling == "weak" else
+                                         "contiguous shards of one global batch)")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "algorithmic_bytes_per_launch": bpp * n,
-                         "kernel_ms": round(kern_ms, 5)},
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": bpp * main_res["points_per_rank"],
+                         "kernel_ms": kern_ms},
+            "collective": coll,
         }
+        if "shards_match_single_projection" in main_res:
+            out["shards_match_single_projection"] = main_res["shards_match_single_projection"]
+        if other is not None:
+            out[other["mode"]] = other
         if not a.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-            res["cpu_baseline"] = cpu_baseline(model_id, params, w, h, n,
+            out["cpu_baseline"] = cpu_baseline(model_id, params, w, h, main_res["points_per_rank"],
                                                a.cpu_baseline_seconds)
+            out["cpu_baseline_o2"] = cpu_baseline(model_id, params, w, h,
+                                                  main_res["points_per_rank"],
+                                                  a.cpu_baseline_seconds / 2, opt="O2")
             thr = host_threads()
             if thr > 1:
-                res["cpu_baseline_all_cores"] = cpu_baseline_all_cores(
-                    model_id, params, w, h, n, a.cpu_baseline_seconds / 2, thr)
-        print(json.dumps(res), flush=True)
+                out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(
+                    model_id, params, w, h, main_res["points_per_rank"],
+                    a.cpu_baseline_seconds / 2, thr)
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -194,6 +194,15 @@ ACM_API int acm_reprojection_stats(const acm_camera *cam, size_t n,
                                    const double *points_2d, double *result,
                                    double *errors, void *workspace,
                                    size_t workspace_bytes, void *stream);
+/* Host-side merge of the results of disjoint shards (the multi-GPU form of
+ * compute_reprojection_error, error_metrics.rs:86-111): parts = nparts x 8
+ * host doubles, each an acm_reprojection_stats result, folded in order --
+ * sums added, extrema combined, (n_valid, mean, n * stddev^2) merged by
+ * Chan's pairwise update -- into result (8 host doubles, same layout).  One
+ * all-gather of the 8 doubles per rank + this merge gives every rank the
+ * same statistics bit for bit.  A point whose error is NaN (failed
+ * projection or NaN observation) is never counted. */
+ACM_API int acm_reprojection_stats_merge(size_t nparts, const double *parts, double *result);
 
 /* linear_estimation (kannala_brandt.rs:164-272, double_sphere.rs:225-290,
  * ucm.rs:200-258, eucm.rs:216-288, rad_tan.rs:153-234).  The 2N x k system

@@ -20,25 +20,29 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+# -O3 build of the same source: the timed CPU baseline (bench.py cpu_baseline)
+_LIB_O3_PATH = os.path.join(_HERE, "build", "liboracle_o3.so")
 
 PINHOLE, RADTAN, KB, DS, UCM, EUCM, FOV = range(7)
 NUM_PARAMS = {PINHOLE: 4, RADTAN: 9, KB: 8, DS: 6, UCM: 5, EUCM: 6, FOV: 5}
 
-_lib = None
+_libs = {}
 
 
 def build() -> str:
-    """Compile liboracle.so (gcc, -ffp-contract=off)."""
+    """Compile liboracle.so and liboracle_o3.so (gcc, -ffp-contract=off)."""
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+def lib(opt: str = "O2"):
+    """The oracle library: opt="O2" (the parity checker) or "O3" (the same
+    source at -O3, the timed CPU baseline)."""
+    path = _LIB_O3_PATH if opt == "O3" else _LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
+        L = ctypes.CDLL(path)
         dp = ctypes.POINTER(ctypes.c_double)
         u8p = ctypes.POINTER(ctypes.c_uint8)
         sz = ctypes.c_size_t
@@ -70,8 +74,8 @@ def lib():
         L.oracle_undistort_image.argtypes = [ctypes.c_int, dp, u32, u32, dp, ctypes.c_int,
                                              u8p, u8p]
         L.oracle_undistort_image.restype = None
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def _dp(a):

@@ -15,6 +15,7 @@ The TCC_EA0_RDREQ/WRREQ pass is kept as a cross-check (x64 B, reads x2).
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 import statistics
@@ -43,6 +44,10 @@ def main():
     ap.add_argument("--points", type=int, required=True)
     ap.add_argument("--algorithmic-bytes", type=int, default=None)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "apex-camera-models_amd", "lib", "libacm.so"),
+        help="the libacm.so the passes ran (its sha256 is recorded: bench.py reports the "
+             "traffic only for that build)")
     a = ap.parse_args()
     by = {}
     for d in sorted(glob.glob(a.prefix + "_*")):
@@ -67,6 +72,7 @@ def main():
         "raw_median": med,
         "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 128-B reads); "
                        "WRITE_SIZE KiB x1024",
+        "libacm_sha256": hashlib.sha256(open(a.lib, "rb").read()).hexdigest(),
     }
     if a.algorithmic_bytes and out["hbm_bytes_per_launch"]:
         out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / a.algorithmic_bytes

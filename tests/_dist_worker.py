@@ -52,6 +52,13 @@ def main():
     stats = D.combine_reprojection_stats(torch.tensor(e))
     out["stats"] = np.array([stats[k] for k in ("rmse", "min", "max", "mean", "stddev",
                                                 "n_valid")])
+    # a shard with no valid error at all (rank 0 here), then every rank's
+    # errors NaN: n_valid 0 on every rank, no division by zero
+    e_mixed = np.full_like(e, np.nan) if rank == 0 else e
+    st_mixed = D.combine_reprojection_stats(torch.tensor(e_mixed))
+    out["stats_mixed"] = np.array([st_mixed[k] for k in D.STAT_KEYS])
+    st_none = D.combine_reprojection_stats(torch.tensor(np.full(5, np.nan)))
+    out["stats_none_n"] = np.array([st_none["n_valid"]])
 
     # --- sharded sample_points (KB, 20k cells) ----------------------------
     kp, (kw, kh) = SAMPLES[2]

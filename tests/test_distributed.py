@@ -38,6 +38,34 @@ def _run(world, tmp_path):
     return [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
 
 
+def test_reprojection_stats_merge_c_abi():
+    """acm_reprojection_stats_merge (host code of libacm.so): merging the
+    shard statistics of a split batch equals the statistics of the whole."""
+    import ctypes
+    import torch
+    from apex_camera_models import _lib
+    from apex_camera_models.distributed import local_reprojection_result
+    rng = np.random.default_rng(3)
+    e = np.abs(rng.normal(1.0, 0.7, 100_003))
+    e[rng.random(e.size) < 0.05] = np.nan
+    whole = local_reprojection_result(e).numpy()
+    for cuts in ([50_000], [0, 10, 99_990], [33_333, 66_666]):
+        parts = np.concatenate([local_reprojection_result(c).numpy()[None]
+                                for c in np.split(e, cuts)])
+        out = (ctypes.c_double * 8)()
+        rc = _lib.load().acm_reprojection_stats_merge(
+            len(parts), parts.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), out)
+        assert rc == 0
+        got = np.array(list(out))
+        assert got[5] == whole[5] and got[1] == whole[1] and got[2] == whole[2]
+        np.testing.assert_allclose(got, whole, rtol=1e-12)
+    out = (ctypes.c_double * 8)()
+    none = np.array([[np.nan, np.inf, -np.inf, np.nan, np.nan, 0, 0, 0]], dtype=np.float64)
+    assert _lib.load().acm_reprojection_stats_merge(
+        1, none.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), out) == 0
+    assert out[5] == 0.0 and np.isnan(out[0])
+
+
 def test_shard_range_partitions():
     from apex_camera_models.distributed import grid_row_range, shard_range
     for n in (0, 1, 7, 10, 10_000_001):
@@ -70,6 +98,18 @@ def test_sharded_exchange_matches_single_process(world, tmp_path):
             assert abs(got[k] - stats[k]) <= 1e-12 * abs(stats[k])
         assert got["min"] == stats["min"] and got["max"] == stats["max"]
     assert all(np.array_equal(res[0]["ne"], r["ne"]) for r in res)
+    # ranks agree bit for bit on the merged statistics (one all-gather +
+    # libacm's rank-ordered Chan merge), also with an all-NaN shard on rank 0
+    assert all(np.array_equal(res[0]["stats"], r["stats"]) for r in res)
+    assert all(np.array_equal(res[0]["stats_mixed"], r["stats_mixed"], equal_nan=True)
+               for r in res)
+    lo, hi = 0, (n + world - 1) // world  # rank 0's shard is excluded in stats_mixed
+    st2, m2 = O.reprojection_error(3, params, w, h, xyz[hi:], obs[hi:])
+    got2 = dict(zip(("rmse", "min", "max", "mean", "stddev", "n_valid"), res[0]["stats_mixed"]))
+    assert got2["n_valid"] == m2
+    for k in ("rmse", "mean", "stddev"):
+        assert abs(got2[k] - st2[k]) <= 1e-12 * abs(st2[k])
+    assert all(int(r["stats_none_n"][0]) == 0 for r in res)
     # sample_points: rank-ordered concatenation == serial order, bit-exact
     kp, (kw, kh) = SAMPLES[2]
     uv_s, xyz_s, _ = O.sample_points(2, kp, kw, kh, 20_000)

@@ -152,6 +152,27 @@ def test_oracle_reproduces_golden(model, golden_dir):
     assert np.array_equal(ray, g["rays"], equal_nan=True)
 
 
+@pytest.mark.parametrize("model", range(7))
+def test_oracle_o3_build_is_bit_identical(model, golden_dir):
+    """bench.py's cpu_baseline times liboracle_o3.so (-O3 -ffp-contract=off,
+    BASELINE.md section 2): it must compute exactly what the -O2 checker does."""
+    g = np.load(os.path.join(golden_dir, f"golden_{model}.npz"))
+    params = g["params"].tolist()
+    w, h = int(g["res"][0]), int(g["res"][1])
+    L = O.lib("O3")
+    xyz = np.ascontiguousarray(g["xyz"])
+    n = xyz.shape[0]
+    P = O.NUM_PARAMS[model]
+    uv = np.empty((n, 2))
+    st = np.empty(n, dtype=np.uint8)
+    J = np.empty((P, n, 2))
+    pa = np.ascontiguousarray(params, dtype=np.float64)
+    L.oracle_project_batch(model, O._dp(pa), w, h, n, O._dp(xyz), O._dp(uv), O._u8p(st), O._dp(J))
+    assert np.array_equal(st, g["proj_status"])
+    assert np.array_equal(uv, g["uv"], equal_nan=True)
+    assert np.array_equal(J, g["jac"], equal_nan=True)
+
+
 def test_rel_err_helper():
     assert rel_err([1.0, np.nan], [1.0, np.nan]) == 0.0
     with pytest.raises(AssertionError):
