@@ -1220,20 +1220,18 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(CamArg cam, Grid g, siz
 // its count computed by the waiting wave itself (tile_keep_count), so no
 // workgroup ever waits on one that has not started.  The kept points come out
 // in cell order exactly as from the two-pass path.
-constexpr int kFusedRMin = 4;  // smallest tile (rounds of 256 cells) any setting uses
-// Per-model tile: fewer, larger tiles mean fewer look-backs, more rays held
-// in registers.  Fastest cell of the
-// interleaved {4, 8, 16} x 256 sweep at 1e8 cells (profiles/r01s7_diag_sample.log).
-template <class TagT> struct SampleR { static constexpr int R = 8; };
-template <> struct SampleR<Tag<Pinhole>> { static constexpr int R = 16; };
-template <> struct SampleR<Tag<Ucm>> { static constexpr int R = 16; };
-template <> struct SampleR<Tag<Eucm>> { static constexpr int R = 16; };
+constexpr int kFusedRMin = 2;  // smallest tile (rounds of 256 cells) any setting uses
+// Per-model tile (rounds of 256 cells): fewer, larger tiles mean fewer
+// look-backs, but each round's rays take 6 KiB of LDS per workgroup, so
+// larger tiles cost occupancy (R = 4: 25 KB, 6 workgroups per CU).
+// ACM_TUNE_SAMPLE_FUSED 1 / 2 / 3 selects R = 2 / 4 / 8.
+template <class TagT> struct SampleR { static constexpr int R = 4; };
 constexpr size_t kFusedCells = (size_t)kBlock * kFusedRMin;
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
 constexpr int kLbPatience = 512;  // polls (s_sleep between) before computing a count itself
 
 template <class TagT, int kFusedR>
-__global__ __launch_bounds__(kBlock) void k_sample_fused(CamArg cam, Grid g, size_t cells,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_sample_fused(CamArg cam, Grid g, size_t cells,
                                                          uint64_t* __restrict__ status,
                                                          double* __restrict__ uv_out,
                                                          double* __restrict__ xyz_out,
@@ -1243,7 +1241,13 @@ __global__ __launch_bounds__(kBlock) void k_sample_fused(CamArg cam, Grid g, siz
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     __shared__ uint64_t s_excl;
     __shared__ uint32_t sm[kFusedR][kBlock / 64];
-    __shared__ double s_xyz[kBlock / 64][64 * 3];  // per-wave store staging (6 KiB)
+    // The rays live in LDS, not in registers: each round's kept rays of a
+    // wave, already compacted (rank order), 1.5 KiB per wave and round.  The
+    // registers then hold only one unprojection's working set, which is what
+    // bounds occupancy during the VALU-heavy phase (rays in VGPRs: 87-119
+    // VGPRs = 4-5 waves/SIMD).
+    __shared__ double s_ray[kFusedR][kBlock / 64][64 * 3];
+    __shared__ uint64_t s_mask[kFusedR][kBlock / 64];  // each wave's kept-lane ballots
     // look-back state that survives the workgroup-wide fallback rounds
     __shared__ uint64_t s_lb_top, s_lb_excl, s_lb_helped, s_lb_help;
     __shared__ uint64_t s_lb_val[64];
@@ -1252,8 +1256,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_fused(CamArg cam, Grid g, siz
     const uint64_t tile = blockIdx.x;
     constexpr size_t kTile = (size_t)kBlock * kFusedR;
     const size_t base = (size_t)tile * kTile;
-    double X[kFusedR], Y[kFusedR], Z[kFusedR];
-    uint64_t m[kFusedR];
+    const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
     if (threadIdx.x == 0) {
         s_lb_top = tile - 1;  // lane l of wave 0 inspects tile top - l
         s_lb_excl = 0;
@@ -1267,32 +1270,34 @@ __global__ __launch_bounds__(kBlock) void k_sample_fused(CamArg cam, Grid g, siz
     uint64_t work = tile;
     uint64_t agg = 0;
     bool published = false;
-#if ACM_DIAG_SAMPLE == 5  // experiment: stagger the first resident batch over ~one tile time
-    if (blockIdx.x < 2048u) {
-        const int k = (int)(blockIdx.x * 7u % 16u);
-        for (int i = 0; i < k; ++i) __builtin_amdgcn_s_sleep(41);
-    }
-#endif
     for (;;) {
         const size_t wbase0 = (size_t)work * kTile;
         CellWalk cw;
         cw.init(g, wbase0 + threadIdx.x);
-#pragma unroll
+#pragma unroll 1
         for (int r = 0; r < kFusedR; ++r, cw.step(g)) {
             const size_t cell = wbase0 + (size_t)r * kBlock + threadIdx.x;
             bool keep = false;
-            double u, v;
-            X[r] = Y[r] = Z[r] = 0.0;
-#if ACM_DIAG_SAMPLE == 2 || ACM_DIAG_SAMPLE == 3  // diagnostic builds: no unprojection
+            double u, v, X = 0.0, Y = 0.0, Z = 0.0;
+#if ACM_DIAG_SAMPLE == 2 || ACM_DIAG_SAMPLE == 3 || ACM_DIAG_SAMPLE == 6  // no unprojection
             u = ((double)cw.j + 0.5) * g.cw;
             v = ((double)cw.i + 0.5) * g.ch;
-            X[r] = u; Y[r] = v; Z[r] = 1.0;
+            X = u; Y = v; Z = 1.0;
             keep = cell < cells && (cw.i + cw.j) % 16 != 0;
 #else
-            if (cell < cells) keep = sample_cell<TagT>(c, g, cw, u, v, X[r], Y[r], Z[r]);
+            if (cell < cells) keep = sample_cell<TagT>(c, g, cw, u, v, X, Y, Z);
 #endif
-            m[r] = __ballot(keep);
-            if (lane == 0) sm[r][wid] = (uint32_t)__popcll(m[r]);
+            const uint64_t mr = __ballot(keep);
+            if (lane == 0) {
+                sm[r][wid] = (uint32_t)__popcll(mr);
+                s_mask[r][wid] = mr;
+            }
+            if (keep) {  // compacted: slot = rank among the wave's kept lanes
+                double* d = s_ray[r][wid] + 3 * __popcll(mr & below);
+                d[0] = X;
+                d[1] = Y;
+                d[2] = Z;
+            }
         }
         __syncthreads();
         uint64_t cnt = 0;
@@ -1313,6 +1318,10 @@ __global__ __launch_bounds__(kBlock) void k_sample_fused(CamArg cam, Grid g, siz
         // Decoupled look-back by wave 0.  A predecessor that has not
         // published after g.patience polls is counted here by the whole
         // workgroup (next pass of the loop); then this tile is recomputed.
+#if ACM_DIAG_SAMPLE == 6  // diagnostic: no look-back at all (wrong offsets; timing only)
+        if (threadIdx.x == 0) s_lb_state = 1;
+        __syncthreads();
+#endif
         if (wid == 0 && __builtin_amdgcn_readfirstlane(s_lb_state) == 0) {
             int64_t top = (int64_t)s_lb_top;
             uint64_t excl = s_lb_excl, helped = s_lb_helped;
@@ -1378,42 +1387,37 @@ __global__ __launch_bounds__(kBlock) void k_sample_fused(CamArg cam, Grid g, siz
     }
     __syncthreads();
     uint64_t run = s_excl;
-    const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
-    double* lx = s_xyz[wid];
     CellWalk cw;
     cw.init(g, base + threadIdx.x);
-#pragma unroll
+#pragma unroll 1
     for (int r = 0; r < kFusedR; ++r, cw.step(g)) {
         uint64_t wbase = run, tot = 0;
         for (int w = 0; w < kBlock / 64; ++w) {
             if (w < wid) wbase += sm[r][w];
             tot += sm[r][w];
         }
-        const uint32_t rank = (uint32_t)__popcll(m[r] & below);
-        const uint32_t cnt = (uint32_t)__popcll(m[r]);
-#if ACM_DIAG_SAMPLE == 1 || ACM_DIAG_SAMPLE == 3  // diagnostic builds: no output stores
-        if (((m[r] >> lane) & 1ull) && X[r] == 1234.5) {
+        const uint64_t mr = s_mask[r][wid];
+        const uint32_t rank = (uint32_t)__popcll(mr & below);
+        const uint32_t cnt = (uint32_t)__popcll(mr);
+#if ACM_DIAG_SAMPLE == 1 || ACM_DIAG_SAMPLE == 3 || ACM_DIAG_SAMPLE == 6  // no output stores
+        (void)rank;
+        (void)cnt;
+        if (((mr >> lane) & 1ull) && s_ray[r][wid][0] == 1234.5) {
+            st2<false>(uv_out, 0.0, 0.0);
+        }
 #else
-        if ((m[r] >> lane) & 1ull) {
-#endif
+        if ((mr >> lane) & 1ull) {
             // the same u, v as sample_cell (point_sampling.rs:69-70): 16 B per
             // lane, consecutive kept points -> one contiguous run per wave
             st2<false>(uv_out + 2 * (wbase + rank), ((double)cw.j + 0.5) * g.cw,
                        ((double)cw.i + 0.5) * g.ch);
-            lx[3 * rank] = X[r];
-            lx[3 * rank + 1] = Y[r];
-            lx[3 * rank + 2] = Z[r];
         }
-        // The wave's kept rays are 3*cnt consecutive doubles of xyz_out: written
-        // from the wave's LDS slab as 16-B pieces on the 16-B grid (plus a single
-        // leading / trailing double) instead of three 8-B stores per lane at a
-        // 24-B stride.  LDS accesses of one wave complete in order; the fences
-        // keep the compiler from moving the reads above the writes.
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#if ACM_DIAG_SAMPLE != 1 && ACM_DIAG_SAMPLE != 3
+        // The wave's kept rays of this round are 3*cnt consecutive doubles of
+        // xyz_out, already compacted in LDS: written as 16-B pieces on the
+        // 16-B grid (plus a single leading / trailing double) instead of
+        // three 8-B stores per lane at a 24-B stride.
         if (cnt) {
+            const double* lx = s_ray[r][wid];
             double* dst = xyz_out + 3 * wbase;
             const uint32_t nd = 3 * cnt;
             const uint32_t h = (uint32_t)((reinterpret_cast<uintptr_t>(dst) >> 3) & 1u);
@@ -1426,9 +1430,6 @@ __global__ __launch_bounds__(kBlock) void k_sample_fused(CamArg cam, Grid g, siz
             if (lane == 63 && ((nd - h) & 1u)) dst[nd - 1] = lx[nd - 1];
         }
 #endif
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // the slab is rewritten next round
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         run += tot;
     }
 }
@@ -2607,11 +2608,11 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
         }
         return dispatch_model(cam->model, [&](auto tag) -> int {
             using TagT = decltype(tag);
-            const int rr = fused == 1 ? 4 : fused == 2 ? 8 : fused == 3 ? 16 : SampleR<TagT>::R;
+            const int rr = fused == 1 ? 2 : fused == 2 ? 4 : fused == 3 ? 8 : SampleR<TagT>::R;
             const size_t ntr = (cells + (size_t)kBlock * rr - 1) / ((size_t)kBlock * rr);
             auto kern = k_sample_fused<TagT, 4>;
+            if (rr == 2) kern = k_sample_fused<TagT, 2>;
             if (rr == 8) kern = k_sample_fused<TagT, 8>;
-            if (rr == 16) kern = k_sample_fused<TagT, 16>;
             hipLaunchKernelGGL(kern, dim3((unsigned)ntr), dim3(kBlock), 0, s, prep(*cam), g, cells,
                                status, points_2d_out, points_3d_out, counts);
             return check_launch("acm_sample_points");

@@ -48,7 +48,7 @@ def main():
                     run(v)
                 e1.record()
                 torch.cuda.synchronize()
-                k = {0: "two_pass", 1: "fused_r4", 2: "fused_r8", 3: "fused_r16"}[v]
+                k = {0: "two_pass", 1: "fused_r2", 2: "fused_r4", 3: "fused_r8"}[v]
                 cells[k] = min(cells.get(k, 1e9), e0.elapsed_time(e1) / 3)
         L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, -1)
         out[mid] = {"kept": kept, "identical": same,
