@@ -47,11 +47,15 @@ int main() {
     acm_sample_points_grid(0, 480, 10, &nx, &ny);
     acm_lm_config cfg;
     acm_lm_default_config(&cfg);
-    for (int key = 0; key < 10; ++key)
+    for (int key = 0; key < 13; ++key)
         for (int v = -3; v < 10; ++v) acm_set_tuning(key, v);
-    for (int key = 0; key < 10; ++key) acm_set_tuning(key, key == 2 || key == 4 ? 0 : -1);
+    for (int key = 0; key < 12; ++key) acm_set_tuning(key, key == 2 || key == 4 ? 0 : -1);
     acm_set_tuning(3, 1);
     acc += acm_normal_equations_workspace_size(2, 12345) + acm_median_workspace_size(999);
+    double parts[16] = {1, 0.1, 2, 1, 0.5, 10, 10, 20, 1, 0.2, 3, 1.2, 0.6, 5, 6, 9}, mres[8];
+    acm_reprojection_stats_merge(2, parts, mres);
+    acm_reprojection_stats_merge(0, nullptr, mres);
+    acc += mres[5];
     printf("ok %d\n", std::isfinite(acc) ? 1 : 0);
     return 0;
 }

@@ -43,3 +43,32 @@ def test_host_c_abi_is_clean_under_asan_ubsan(tmp_path):
     assert r.returncode == 0, r.stderr[-4000:]
     assert r.stdout.startswith("ok"), r.stdout
     assert "runtime error" not in r.stderr, r.stderr[-4000:]
+
+
+def _compile_tsan(src, out):
+    return subprocess.Popen([HIPCC, "--offload-arch=gfx950", "-O1", "-std=c++17",
+                             "-ffp-contract=off", "-fPIC", "-Xarch_host", "-g", "-Xarch_host",
+                             "-fsanitize=thread", "-Xarch_device", "-O0", "-I",
+                             os.path.join(ROOT, "include"), "-c",
+                             os.path.join(PKG, "csrc", src), "-o", out])
+
+
+@pytest.mark.skipif(not (os.path.exists(HIPCC) and os.path.exists(CLANG)), reason="no ROCm")
+def test_host_c_abi_is_race_free_under_tsan(tmp_path):
+    """Threads race acm_set_tuning (every knob is a std::atomic) against the
+    host-side entry points (tests/capi_tsan_driver.cpp): ThreadSanitizer must
+    report nothing."""
+    objs = [str(tmp_path / "acm_tsan.o"), str(tmp_path / "solver_tsan.o")]
+    procs = [_compile_tsan("acm.hip", objs[0]), _compile_tsan("solver.hip", objs[1])]
+    assert [p.wait(timeout=600) for p in procs] == [0, 0]
+    exe = str(tmp_path / "capi_tsan")
+    subprocess.run([CLANG, "-g", "-std=c++17", "-fsanitize=thread", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "capi_tsan_driver.cpp"), *objs,
+                    "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lamdhip64", "-o", exe],
+                   check=True)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:report_signal_unsafe=0")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert r.stdout.startswith("ok 1"), r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]

@@ -278,7 +278,7 @@ def test_sample_points_vs_oracle(model, n):
 
 @pytest.mark.parametrize("model", range(7))
 def test_sample_points_every_path_matches_oracle(model):
-    """The single-pass look-back kernel at every tile size (4/8/16 x 256
+    """The single-pass look-back kernel at every tile size (2/4/8 x 256
     cells, ~500 tiles, a ragged last tile) and the two-pass path give the
     oracle's kept set in the oracle's order, bit for bit, and a row-range
     shard of the grid (odd cell offset) matches its slice of the full run."""
@@ -490,3 +490,24 @@ def test_median_radix_select_exact(case):
         assert np.isnan(got)
     else:
         assert got == np.median(valid), (got, np.median(valid))
+
+
+def test_status_on_thresholds_matches_oracle(be):
+    """tests/boundary_probes.py: +-8 ulps around every threshold root; the
+    kernels' statuses equal the oracle's (which test_boundaries.py pins to a
+    binary64 emulation of the Rust conditions), values bit-exact for the
+    models without a transcendental and within 1e-10 for KB."""
+    import boundary_probes as B
+    for model, p, (w, h), kind, pts in B.probes():
+        if kind == "project":
+            uv, st, _ = be.project(model, p, w, h, pts, want_jac=False)
+            uv0, st0, _ = O.project(model, p, w, h, pts)
+        else:
+            uv, st = be.unproject(model, p, w, h, pts)
+            uv0, st0 = O.unproject(model, p, w, h, pts)
+        assert np.array_equal(st, st0), (model, kind, np.nonzero(st != st0)[0][:5])
+        ok = st0 == 0
+        if model == 2:
+            assert rel_err(uv[ok], uv0[ok], floor=1.0) <= TOL
+        else:
+            assert np.array_equal(uv[ok], uv0[ok]), (model, kind)
