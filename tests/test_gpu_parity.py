@@ -510,4 +510,4 @@ def test_status_on_thresholds_matches_oracle(be):
         if model == 2:
             assert rel_err(uv[ok], uv0[ok], floor=1.0) <= TOL
         else:
-            assert np.array_equal(uv[ok], uv0[ok]), (model, kind)
+            assert np.array_equal(uv[ok], uv0[ok], equal_nan=True), (model, kind)
