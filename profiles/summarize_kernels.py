@@ -24,6 +24,7 @@ import csv
 import glob
 import json
 import os
+import re
 
 FP64_PEAK_TF = 78.6
 HBM_PEAK_GBS = 8000.0
@@ -32,7 +33,8 @@ SIMDS = 1024
 
 def short(name):
     n = name.split("(")[0].replace("void ", "").replace("acm::", "")
-    return n.replace("Tag<", "").replace(">", "").replace("<", "[").replace(", ", ",")[:60]
+    n = re.sub(r"Tag<(\w+)>", r"\1", n)
+    return n.replace(", ", ",")[:70]
 
 
 def main():
@@ -47,7 +49,6 @@ def main():
                                      "avg_us": float(r["AverageNs"]) / 1e3,
                                      "min_us": float(r["MinNs"]) / 1e3}
     ctr = collections.defaultdict(lambda: collections.defaultdict(list))
-    kdur = collections.defaultdict(list)
     for d in sorted(glob.glob(f"{a.prefix}_pmc*")):
         if not os.path.isdir(d):
             continue

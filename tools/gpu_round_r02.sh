@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round measurement call: GPU tests, smoke, bench line, rocprofv3 kernel trace
+# of the bench, the headline PMC passes (traffic), the FP64-kernel counter
+# passes, every SURVEY 8(a) row beside the oracle, configs 1/3/4/5 and the
+# sample_points variants.  Every step has its own time limit; a crash or
+# timeout (rc > 1) ends the script.
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r02}
+check() { local rc=$1 name=$2; echo "$name rc=$rc"; if [ "$rc" -gt 1 ]; then echo "stopping after $name"; exit "$rc"; fi; }
+if [ -z "${SKIP_TESTS:-}" ]; then
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf > gpurun_out/${TAG}_pytest_gpu.log 2>&1
+check $? pytest; tail -n 2 gpurun_out/${TAG}_pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1
+check $? smoke; tail -n 1 gpurun_out/${TAG}_smoke.log
+fi
+timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.log 2>&1
+check $? bench
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o kt \
+  -- python3 bench.py --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1
+check $? rocprof
+TAG=${TAG} bash tools/pmc_round.sh > gpurun_out/${TAG}_pmc_round.log 2>&1
+check $? pmc_round
+TAG=${TAG} bash tools/pmc_fp64.sh > gpurun_out/${TAG}_pmc_fp64.log 2>&1
+check $? pmc_fp64
+timeout -k 10 400 python tools/bench_rows.py > gpurun_out/${TAG}_rows.log 2>&1
+check $? rows
+timeout -k 10 400 python tools/bench_configs.py --configs 1,3,4,5 > gpurun_out/${TAG}_configs.log 2>&1
+check $? configs
+timeout -k 10 300 python tools/diag_sample.py > gpurun_out/${TAG}_diag_sample.log 2>&1
+check $? diag_sample
+echo done
