@@ -1072,16 +1072,28 @@ struct Grid {
     int patience;  // look-back polls before counting a predecessor's cells itself
 };
 
-// Row/column of a cell, advanced incrementally: one 64-bit division per lane
-// per workgroup (at the first cell it visits), then each step of kBlock cells
-// is an add and (for ncx >= kBlock) at most one wrap -- instead of a 64-bit
-// division and remainder (a ~50-instruction VALU sequence) per cell.
+// 64-bit value known to be wave-uniform, moved to SGPRs (so arithmetic on
+// it runs on the scalar unit).
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+
+// Row/column of a cell, advanced incrementally.  init() divides the
+// workgroup-uniform first cell of a tile once, on the scalar unit, and each
+// lane adds its offset (< kBlock) with a wrap; each step of kBlock cells is
+// an add and (for ncx >= kBlock) at most one wrap.  A per-lane 64-bit
+// division and remainder is a ~60-instruction VALU sequence: done per lane
+// at the start of every tile's compute and store passes it cost ~30 VALU
+// instructions per 64 cells.
 struct CellWalk {
     uint32_t i, j;
-    __device__ __forceinline__ void init(const Grid& g, size_t cell) {
-        cell += g.cell0;
-        i = (uint32_t)(cell / g.ncx);
-        j = (uint32_t)(cell - (size_t)i * g.ncx);
+    __device__ __forceinline__ void init(const Grid& g, uint64_t base, uint32_t off) {
+        const uint64_t cb = uniform64(base + g.cell0);
+        const uint64_t i0 = cb / g.ncx;
+        i = (uint32_t)i0;
+        j = (uint32_t)(cb - i0 * g.ncx) + off;
+        while (j >= g.ncx) { j -= g.ncx; ++i; }
     }
     __device__ __forceinline__ void step(const Grid& g) {
         j += kBlock;
@@ -1114,7 +1126,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_count(CamArg cam, Grid g, siz
     const size_t base = (size_t)blockIdx.x * kSampleCells;
     uint32_t mine = 0;
     CellWalk cw;
-    cw.init(g, base + threadIdx.x);
+    cw.init(g, base, threadIdx.x);
     for (int r = 0; r < kSampleR; ++r, cw.step(g)) {
         const size_t cell = base + (size_t)r * kBlock + threadIdx.x;
         if (cell < cells) {
@@ -1180,7 +1192,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(CamArg cam, Grid g, siz
     const size_t base = (size_t)blockIdx.x * kSampleCells;
     uint64_t run = offsets[blockIdx.x];
     CellWalk cw;
-    cw.init(g, base + threadIdx.x);
+    cw.init(g, base, threadIdx.x);
     for (int r = 0; r < kSampleR; ++r, cw.step(g)) {
         const size_t cell = base + (size_t)r * kBlock + threadIdx.x;
         bool keep = false;
@@ -1230,6 +1242,15 @@ constexpr size_t kFusedCells = (size_t)kBlock * kFusedRMin;
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
 constexpr int kLbPatience = 512;  // polls (s_sleep between) before computing a count itself
 
+#if ACM_DIAG_SAMPLE == 7
+// Diagnostic build only: one record per tile -- wall clock (100 MHz) at
+// entry, after the first compute pass, after the look-back, after the stores
+// were issued; look-back loads, loads that found a nearer tile unpublished,
+// 64-tile windows walked, fallback (help) passes.
+constexpr size_t kDiagRecs = 1u << 18;
+__device__ unsigned long long g_sample_rec[kDiagRecs][8];
+#endif
+
 template <class TagT, int kFusedR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_sample_fused(CamArg cam, Grid g, size_t cells,
                                                          uint64_t* __restrict__ status,
@@ -1251,7 +1272,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     // look-back state that survives the workgroup-wide fallback rounds
     __shared__ uint64_t s_lb_top, s_lb_excl, s_lb_helped, s_lb_help;
     __shared__ uint64_t s_lb_val[64];
-    __shared__ uint32_t s_lb_cnt[kBlock / 64];
     __shared__ int s_lb_state;
     const uint64_t tile = blockIdx.x;
     constexpr size_t kTile = (size_t)kBlock * kFusedR;
@@ -1270,10 +1290,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     uint64_t work = tile;
     uint64_t agg = 0;
     bool published = false;
+#if ACM_DIAG_SAMPLE == 7
+    const long long d_t0 = wall_clock64();
+    long long d_t1 = 0;
+    unsigned long long d_polls = 0, d_waits = 0, d_windows = 0, d_helps = 0;
+#endif
     for (;;) {
         const size_t wbase0 = (size_t)work * kTile;
         CellWalk cw;
-        cw.init(g, wbase0 + threadIdx.x);
+        cw.init(g, wbase0, threadIdx.x);
 #pragma unroll 1
         for (int r = 0; r < kFusedR; ++r, cw.step(g)) {
             const size_t cell = wbase0 + (size_t)r * kBlock + threadIdx.x;
@@ -1315,11 +1340,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
             s_lb_helped |= 1ull << l;
         }
         __syncthreads();
+#if ACM_DIAG_SAMPLE == 7
+        if (d_t1 == 0) d_t1 = wall_clock64();
+#endif
         // Decoupled look-back by wave 0.  A predecessor that has not
         // published after g.patience polls is counted here by the whole
         // workgroup (next pass of the loop); then this tile is recomputed.
 #if ACM_DIAG_SAMPLE == 6  // diagnostic: no look-back at all (wrong offsets; timing only)
         if (threadIdx.x == 0) s_lb_state = 1;
+        __syncthreads();
+#endif
+#if ACM_DIAG_SAMPLE == 8  // diagnostic: full compute and stores, no look-back: each
+        // tile writes at 15/16 of its cell offset (in bounds: the outputs hold
+        // one slot per cell; wrong offsets, timing only)
+        if (threadIdx.x == 0) {
+            s_lb_excl = tile * kTile - (tile * kTile) / 16;
+            s_lb_state = 1;
+        }
         __syncthreads();
 #endif
         if (wid == 0 && __builtin_amdgcn_readfirstlane(s_lb_state) == 0) {
@@ -1332,11 +1369,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
                                                           __HIP_MEMORY_SCOPE_AGENT)
                                       : kLbIncl;  // before tile 0: prefix 0
                 if (((helped >> lane) & 1ull) && (w >> 62) == 0) w = help_w;
+#if ACM_DIAG_SAMPLE == 7
+                ++d_polls;
+#endif
                 const uint64_t incl = __ballot((w >> 62) == 2);
                 const uint64_t none = __ballot((w >> 62) == 0);
                 const int stop = incl ? __ffsll((long long)incl) - 1 : 64;
                 const uint64_t need = stop == 63 || stop == 64 ? ~0ull : ((2ull << stop) - 1);
                 if (none & need) {  // a nearer tile has not published yet
+#if ACM_DIAG_SAMPLE == 7
+                    ++d_waits;
+#endif
                     if (++polls < g.patience) {
                         __builtin_amdgcn_s_sleep(2);
                         continue;
@@ -1365,12 +1408,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
                 top -= 64;
                 helped = 0;
                 polls = 0;
+#if ACM_DIAG_SAMPLE == 7
+                ++d_windows;
+#endif
             }
         }
         __syncthreads();
         const int state = __builtin_amdgcn_readfirstlane(s_lb_state);
         if (state == 1 && work == tile) break;  // prefix known, own rays in registers
         if (state == 2) {
+#if ACM_DIAG_SAMPLE == 7
+            ++d_helps;
+#endif
             work = s_lb_top - s_lb_help;
             __syncthreads();  // everyone has read the request before it is reset
             if (threadIdx.x == 0) s_lb_state = 0;
@@ -1386,9 +1435,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         }
     }
     __syncthreads();
+#if ACM_DIAG_SAMPLE == 7
+    const long long d_t2 = wall_clock64();
+#endif
     uint64_t run = s_excl;
     CellWalk cw;
-    cw.init(g, base + threadIdx.x);
+    cw.init(g, base, threadIdx.x);
 #pragma unroll 1
     for (int r = 0; r < kFusedR; ++r, cw.step(g)) {
         uint64_t wbase = run, tot = 0;
@@ -1432,6 +1484,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
 #endif
         run += tot;
     }
+#if ACM_DIAG_SAMPLE == 7
+    if (threadIdx.x == 0 && tile < kDiagRecs) {
+        unsigned long long* rec = g_sample_rec[tile];
+        rec[0] = d_t0;
+        rec[1] = d_t1;
+        rec[2] = d_t2;
+        rec[3] = wall_clock64();
+        rec[4] = d_polls;
+        rec[5] = d_waits;
+        rec[6] = d_windows;
+        rec[7] = d_helps;
+    }
+#endif
 }
 
 // ----------------------------------------------------------------- median
@@ -2135,6 +2200,13 @@ using namespace acm;
 
 // ====================================================================== C-ABI
 extern "C" {
+#if ACM_DIAG_SAMPLE == 7
+ACM_API int acm_diag_sample_records(void* host, size_t bytes) {
+    if (bytes > sizeof(g_sample_rec)) bytes = sizeof(g_sample_rec);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sample_rec), bytes, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
+}
+#endif
 
 ACM_API int acm_num_params(int model) {
     switch (model) {

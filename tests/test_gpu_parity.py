@@ -309,12 +309,33 @@ def test_sample_points_every_path_matches_oracle(model):
         L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, -1)
 
 
+def test_sample_points_kb_clamped_angle():
+    """KB with no distortion and a short focal length: every pixel with
+    ru >= pi/2 clamps to theta = 1.5707963267948966 (kannala_brandt.rs:467)
+    and Newton stays there, so Z = cos(theta) / |p| is +6.1e-17 / |p| -- kept
+    (point_sampling.rs:91-94) -- while the next double up would be dropped.
+    The keep decision at that exact angle, and the kept set around it, must
+    match the oracle (glibc cos)."""
+    from apex_camera_models import util
+    params = [100.0, 100.0, 320.0, 240.0, 0.0, 0.0, 0.0, 0.0]
+    w, h = 640, 480
+    m = _model_obj(2, params, w, h)
+    for n in (5000, 300_000):
+        uv, xyz = util.sample_points(m, n)
+        uv0, xyz0, _ = O.sample_points(2, params, w, h, n)
+        assert np.array_equal(uv.cpu().numpy(), uv0)
+        assert rel_err(xyz.cpu().numpy(), xyz0, floor=1.0) <= TOL
+        # the clamped pixels are there (Z tiny but positive)
+        assert (xyz0[:, 2] < 1e-15).sum() > 0
+
+
+@pytest.mark.parametrize("fused", [1, 2, 3])
 @pytest.mark.parametrize("model", [1, 2, 4])
-def test_sample_points_lookback_fallback(model):
+def test_sample_points_lookback_fallback(model, fused):
     """ACM_TUNE_SAMPLE_PATIENCE = 0: a tile whose predecessor has not yet
     published its count counts that predecessor's cells itself at once (the
-    path that guarantees progress whatever the dispatch order).  Outputs stay
-    bit-identical to the default run and the oracle."""
+    path that guarantees progress whatever the dispatch order), at every tile
+    size.  Outputs stay bit-identical to the default run and the oracle."""
     from apex_camera_models import _lib, util
     from test_oracle import SAMPLES
     params, (w, h) = SAMPLES[model]
@@ -323,12 +344,14 @@ def test_sample_points_lookback_fallback(model):
     L = _lib.load()
     uv_d, xyz_d = util.sample_points(m, n)
     try:
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, fused)
         L.acm_set_tuning(_lib.TUNE_SAMPLE_PATIENCE, 0)
         for _ in range(3):
             uv, xyz = util.sample_points(m, n)
             assert torch_equal_bits(uv, uv_d) and torch_equal_bits(xyz, xyz_d)
     finally:
         L.acm_set_tuning(_lib.TUNE_SAMPLE_PATIENCE, -1)
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, -1)
     uv0, xyz0, _ = O.sample_points(model, params, w, h, n)
     assert np.array_equal(uv.cpu().numpy(), uv0)
 

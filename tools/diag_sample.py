@@ -25,7 +25,7 @@ def main():
     names = ["pinhole", "rad_tan", "kannala_brandt", "double_sphere", "ucm", "eucm", "fov"]
     L = _lib.load()
     out = {}
-    for mid in range(7):
+    for mid in [int(x) for x in os.environ.get("MODELS", "0,1,2,3,4,5,6").split(",")]:
         params, (w, h) = samples.SAMPLES[mid]
         m = MODEL_CLASSES[names[mid]]._from_params([float(p) for p in params], Resolution(w, h))
 
@@ -33,13 +33,14 @@ def main():
             L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, v)
             return util.sample_points(m, a.cells)
 
-        res = {v: run(v) for v in (0, 1, 2, 3)}
-        same = all(torch.equal(res[0][k], res[v][k]) for k in (0, 1) for v in (1, 2, 3))
-        kept = int(res[1][0].shape[0])
+        VS = [int(x) for x in os.environ.get("VARIANTS", "0,1,2,3").split(",")]
+        res = {v: run(v) for v in VS}
+        same = all(torch.equal(res[VS[0]][k], res[v][k]) for k in (0, 1) for v in VS)
+        kept = int(res[VS[0]][0].shape[0])
         del res
         cells = {}
         for _ in range(3):
-            for v in (0, 1, 2, 3):
+            for v in VS:
                 run(v)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
