@@ -1252,7 +1252,7 @@ __device__ unsigned long long g_sample_rec[kDiagRecs][8];
 #endif
 
 template <class TagT, int kFusedR>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_sample_fused(CamArg cam, Grid g, size_t cells,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR >= 8 ? 3 : 6))) void k_sample_fused(CamArg cam, Grid g, size_t cells,
                                                          uint64_t* __restrict__ status,
                                                          double* __restrict__ uv_out,
                                                          double* __restrict__ xyz_out,

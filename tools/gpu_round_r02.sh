@@ -30,4 +30,6 @@ timeout -k 10 400 python tools/bench_configs.py --configs 1,3,4,5 > gpurun_out/$
 check $? configs
 timeout -k 10 300 python tools/diag_sample.py > gpurun_out/${TAG}_diag_sample.log 2>&1
 check $? diag_sample
+timeout -k 10 300 python tools/bench_e2e.py > gpurun_out/${TAG}_e2e.log 2>&1
+check $? e2e
 echo done
