@@ -135,6 +135,9 @@ EXPORTED_SYMBOLS = (
 _lib = None
 
 
+from ._buildinfo import source_sha256  # noqa: E402,F401  (bench.py's traffic check)
+
+
 class AcmError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"libacm error {code}: {msg}")

@@ -19,6 +19,14 @@ import hashlib
 import json
 import os
 import statistics
+import importlib.util
+
+_BI = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "apex-camera-models_amd", "apex_camera_models", "_buildinfo.py")
+_spec = importlib.util.spec_from_file_location("_acm_buildinfo", _BI)
+_buildinfo = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(_buildinfo)
+source_sha256 = _buildinfo.source_sha256
 
 
 def read_counters(d, kernel_pat):
@@ -73,6 +81,7 @@ def main():
         "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 128-B reads); "
                        "WRITE_SIZE KiB x1024",
         "libacm_sha256": hashlib.sha256(open(a.lib, "rb").read()).hexdigest(),
+        "libacm_source_sha256": source_sha256(),
     }
     if a.algorithmic_bytes and out["hbm_bytes_per_launch"]:
         out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / a.algorithmic_bytes
