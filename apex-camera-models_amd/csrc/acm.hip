@@ -1238,6 +1238,13 @@ constexpr int kFusedRMin = 2;  // smallest tile (rounds of 256 cells) any settin
 // larger tiles cost occupancy (R = 4: 25 KB, 6 workgroups per CU).
 // ACM_TUNE_SAMPLE_FUSED 1 / 2 / 3 selects R = 2 / 4 / 8.
 template <class TagT> struct SampleR { static constexpr int R = 4; };
+// Auto (-1) picks the single pass for every model whose unprojection is
+// worth computing once, and the two-pass path for Pinhole: its unprojection
+// is a sqrt and a division, so counting and recomputing costs less than the
+// look-back and the LDS staging (0.99-1.04 vs 1.14-1.16 ms at 1e8 cells;
+// profiles/r02_diag_sample.log, r02b_diag_sample.log).
+template <class TagT> struct SampleSinglePass { static constexpr bool on = true; };
+template <> struct SampleSinglePass<Tag<Pinhole>> { static constexpr bool on = false; };
 constexpr size_t kFusedCells = (size_t)kBlock * kFusedRMin;
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
 constexpr int kLbPatience = 512;  // polls (s_sleep between) before computing a count itself
@@ -2668,7 +2675,10 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
     hipStream_t s = (hipStream_t)stream;
     // (plain stores: non-temporal ones measured slower for these compacted
     // outputs, 1.41 -> 1.47 ms at 1e8 KB cells, profiles/r02_diag_sample_phases.log)
-    const int fused = g_sample_fused;
+    int fused = g_sample_fused;
+    if (fused < 0 && cam->model == ACM_PINHOLE &&
+        !SampleSinglePass<Tag<Pinhole>>::on)
+        fused = 0;
     if (fused != 0) {
         uint64_t* status = (uint64_t*)workspace + 1;
         if (hipMemsetAsync(workspace, 0, (nt + 1) * sizeof(uint64_t), s) != hipSuccess)

@@ -401,8 +401,10 @@ ACM_API int acm_stream_synchronize(void *stream);
  * word the kernel publishes; -1 = auto = 2.
  * ACM_TUNE_SAMPLE_FUSED: acm_sample_points in one pass (unproject once,
  * decoupled look-back for the output offsets; -1 = auto = tiles of 4 x 256
- * cells, 1 / 2 / 3 = tiles of 2 / 4 / 8 x 256 cells) or the two-pass count /
- * scan / recompute-and-write path (0).
+ * cells for every model but Pinhole, whose unprojection is cheap enough
+ * that the two-pass path is faster; 1 / 2 / 3 = tiles of 2 / 4 / 8 x 256
+ * cells) or the two-pass count / scan / recompute-and-write path (0).
+ * Outputs are identical for every value.
  * ACM_TUNE_UNPROJECT_RCP: unprojections (acm_unproject, acm_sample_points*)
  * divide by fx, fy through the host's correctly rounded 1/fx, 1/fy and one
  * FMA correction, bit-identical to the division (-1 = auto = on, 0 = plain
