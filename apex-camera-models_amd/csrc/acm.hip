@@ -505,6 +505,68 @@ __global__ __launch_bounds__(kBlock) void k_unproject(CamArg cam, size_t n,
     st1<NT>(status + i, st);
 }
 
+#ifdef ACM_DIAG_REFILL
+// Diagnostic build (ACM_DIAG_REFILL = K): RadTan acm_unproject with lane
+// refill.  Each wave owns a contiguous chunk of pixels; a lane whose Newton
+// loop has ended writes its ray and status and, once at least K lanes of
+// the wave are idle, the idle lanes take the next pixels of the chunk (in
+// lane order, so the refill loads are contiguous).  Per-point iterates are
+// RadTan::newton_step's, so outputs are bit-identical to k_unproject.
+template <int K>
+__global__ __launch_bounds__(kBlock) void k_unproject_refill(CamArg cam, size_t n,
+                                                             size_t chunk,
+                                                             const double* __restrict__ uv,
+                                                             double* __restrict__ rays,
+                                                             uint8_t* __restrict__ status) {
+    using M = RadTan<double>;
+    const Cam<double> c = make_cam<double>(cam);
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
+    const size_t wave = (size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const size_t begin = wave * chunk;
+    const size_t end = begin + chunk < n ? begin + chunk : n;
+    size_t head = begin;
+    size_t idx = 0;
+    bool active = false;
+    M::Newton st;
+    for (;;) {
+        const uint64_t idle = __ballot(!active);
+        if (head < end && (size_t)__popcll(idle) >= (size_t)K) {
+            const size_t cand = head + (size_t)__popcll(idle & below);
+            head += (size_t)__popcll(idle);
+            if (!active && cand < end) {
+                idx = cand;
+                const double2 q = *reinterpret_cast<const double2*>(uv + 2 * idx);
+                if (M::newton_init(c, q.x, q.y, st)) {
+                    active = true;
+                } else {  // outside the image: NaN ray at once
+                    const double nn = __builtin_nan("");
+                    rays[3 * idx] = nn;
+                    rays[3 * idx + 1] = nn;
+                    rays[3 * idx + 2] = nn;
+                    status[idx] = st.st;
+                }
+            }
+            continue;  // re-count: a lane that got an out-of-image pixel is idle again
+        }
+        if (!__ballot(active)) {
+            if (head >= end) break;
+            continue;
+        }
+        if (active && M::newton_step(c, st)) {
+            double X, Y, Z;
+            const uint8_t r = M::newton_finish(st, X, Y, Z);
+            if (r != ST_OK) X = Y = Z = __builtin_nan("");
+            rays[3 * idx] = X;
+            rays[3 * idx + 1] = Y;
+            rays[3 * idx + 2] = Z;
+            status[idx] = r;
+            active = false;
+        }
+    }
+}
+#endif
+
 // -------------------------------------------------- residual + Jacobian
 template <class TagT, int LAYOUT, bool WJ, bool NT>
 __global__ __launch_bounds__(kBlock) void k_residual(acm_camera cam, size_t n,
@@ -2400,6 +2462,17 @@ ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_
         const dim3 g(grid_for(n)), b(kBlock);
         const bool nt = n * 25 > kNtThresholdBytes;  // rays + status written once
         const bool ntl = g_nt_loads_unproject == 1;
+#ifdef ACM_DIAG_REFILL
+        if (std::is_same<TagT, Tag<RadTan>>::value && layout == ACM_LAYOUT_AOS) {
+            auto kern = k_unproject_refill<ACM_DIAG_REFILL>;
+            const size_t waves = (size_t)resident_blocks((const void*)kern) * (kBlock / 64);
+            const size_t chunk = (n + waves - 1) / waves;
+            const size_t blocks = ((n + chunk - 1) / chunk + kBlock / 64 - 1) / (kBlock / 64);
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), b, 0, s, prep(*cam), n, chunk,
+                               points_2d, rays, status);
+            return check_launch("acm_unproject");
+        }
+#endif
         auto go = [&](auto lay_c) {
             constexpr int L = decltype(lay_c)::value;
             auto kern = nt ? (ntl ? k_unproject<TagT, L, true, true> : k_unproject<TagT, L, true, false>)

@@ -345,64 +345,91 @@ struct RadTan {
         }
         return st;
     }
-    // rad_tan.rs:401-524: Newton on the 2x2 distortion Jacobian, <=100 steps.
-    __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
-                                                        T& Z) {
+    // rad_tan.rs:401-524: Newton on the 2x2 distortion Jacobian, <=100 steps,
+    // split into init / step / finish so a lane-refill kernel can run the
+    // same per-point iterates (k_unproject_refill); unproject() chains them.
+    struct Newton {
+        T tx, ty, px, py;
+        unsigned it;
+        uint8_t st;
+    };
+    // :401-433; false when the pixel is outside the image (the ray is NaN)
+    __device__ static __forceinline__ bool newton_init(const Cam<T>& c, T u, T v, Newton& s) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
-        const T k1 = c.p[4], k2 = c.p[5], p1 = c.p[6], p2 = c.p[7], k3 = c.p[8];
         if (u < T(0) || u >= c.w || v < T(0) || v >= c.h) {
-            X = Y = Z = T(NAN);
-            return ST_POINT_IS_OUT_SIDE_IMAGE;
+            s.st = ST_POINT_IS_OUT_SIDE_IMAGE;
+            return false;
         }
-        const T tx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
-        const T ty = div_by_f(v - cy, fy, c.ify);
-        T px = tx, py = ty;
-        uint8_t st = ST_OK;
-        for (unsigned it = 0; it < 100u; ++it) {
-            T x = px, y = py;
-            T r2 = x * x + y * y;
-            T r4 = r2 * r2;
-            T r6 = r4 * r2;
-            T rad = T(1) + k1 * r2 + k2 * r4 + k3 * r6;
-            T xe = x * rad + T(2) * p1 * x * y + p2 * (r2 + T(2) * x * x);
-            T ye = y * rad + p1 * (r2 + T(2) * y * y) + T(2) * p2 * x * y;
-            T ex = xe - tx, ey = ye - ty;
-            // A NaN error can never pass the two EPS tests nor make det == 0,
-            // so the reference would spin to MAX_ITERATIONS and return
-            // NumericalError (:514-520): stop now with the same outcome.  This
-            // keeps NaN/inf pixels (0.1% of the bench cloud) from holding
-            // their whole wave for 100 iterations.
-            if (ex != ex || ey != ey) { st = ST_NUMERICAL_ERROR; break; }
-            if (norm_below_1e6(ex * ex + ey * ey)) break;  // :459, sqrt(.) < EPS
-            T drdx = T(2) * x, drdy = T(2) * y;
-            T ddx = (k1 + T(2) * k2 * r2 + T(3) * k3 * r4) * drdx;
-            T ddy = (k1 + T(2) * k2 * r2 + T(3) * k3 * r4) * drdy;
-            T j00 = rad + x * ddx + T(2) * p1 * y + p2 * (drdx + T(4) * x);
-            T j01 = x * ddy + T(2) * p1 * x + p2 * (drdy);
-            T j10 = y * ddx + p1 * (drdx) + T(2) * p2 * y;
-            T j11 = rad + y * ddy + p1 * (drdy + T(4) * y) + T(2) * p2 * x;
-            // nalgebra Matrix2::try_inverse: det = m11*m22 - m21*m12
-            T det = j00 * j11 - j10 * j01;
-            if (det == T(0)) { st = ST_NUMERICAL_ERROR; break; }
-            const T nq[4] = {j11, -j01, -j10, j00};
-            T inv[4];
-            div_shared(nq, det, inv);  // = j11 / det, -j01 / det, -j10 / det, j00 / det
-            T i00 = inv[0], i01 = inv[1];
-            T i10 = inv[2], i11 = inv[3];
-            T dx = i00 * ex + i01 * ey;
-            T dy = i10 * ex + i11 * ey;
-            px = px - dx;
-            py = py - dy;
-            if (norm_below_1e6(dx * dx + dy * dy)) break;  // :503, sqrt(.) < EPS
-            if (it == 99u) st = ST_NUMERICAL_ERROR;    // :514
-        }
-        T n = sqrt(px * px + py * py + T(1) * T(1));
-        const T nq[2] = {px, py};
+        s.tx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
+        s.ty = div_by_f(v - cy, fy, c.ify);
+        s.px = s.tx;
+        s.py = s.ty;
+        s.it = 0;
+        s.st = ST_OK;
+        return true;
+    }
+    // one pass of the loop at :436-518; true when the loop has ended
+    __device__ static __forceinline__ bool newton_step(const Cam<T>& c, Newton& s) {
+        const T k1 = c.p[4], k2 = c.p[5], p1 = c.p[6], p2 = c.p[7], k3 = c.p[8];
+        T x = s.px, y = s.py;
+        T r2 = x * x + y * y;
+        T r4 = r2 * r2;
+        T r6 = r4 * r2;
+        T rad = T(1) + k1 * r2 + k2 * r4 + k3 * r6;
+        T xe = x * rad + T(2) * p1 * x * y + p2 * (r2 + T(2) * x * x);
+        T ye = y * rad + p1 * (r2 + T(2) * y * y) + T(2) * p2 * x * y;
+        T ex = xe - s.tx, ey = ye - s.ty;
+        // A NaN error can never pass the two EPS tests nor make det == 0,
+        // so the reference would spin to MAX_ITERATIONS and return
+        // NumericalError (:514-520): stop now with the same outcome.  This
+        // keeps NaN/inf pixels (0.1% of the bench cloud) from holding
+        // their whole wave for 100 iterations.
+        if (ex != ex || ey != ey) { s.st = ST_NUMERICAL_ERROR; return true; }
+        if (norm_below_1e6(ex * ex + ey * ey)) return true;  // :459, sqrt(.) < EPS
+        T drdx = T(2) * x, drdy = T(2) * y;
+        T ddx = (k1 + T(2) * k2 * r2 + T(3) * k3 * r4) * drdx;
+        T ddy = (k1 + T(2) * k2 * r2 + T(3) * k3 * r4) * drdy;
+        T j00 = rad + x * ddx + T(2) * p1 * y + p2 * (drdx + T(4) * x);
+        T j01 = x * ddy + T(2) * p1 * x + p2 * (drdy);
+        T j10 = y * ddx + p1 * (drdx) + T(2) * p2 * y;
+        T j11 = rad + y * ddy + p1 * (drdy + T(4) * y) + T(2) * p2 * x;
+        // nalgebra Matrix2::try_inverse: det = m11*m22 - m21*m12
+        T det = j00 * j11 - j10 * j01;
+        if (det == T(0)) { s.st = ST_NUMERICAL_ERROR; return true; }
+        const T nq[4] = {j11, -j01, -j10, j00};
+        T inv[4];
+        div_shared(nq, det, inv);  // = j11 / det, -j01 / det, -j10 / det, j00 / det
+        T i00 = inv[0], i01 = inv[1];
+        T i10 = inv[2], i11 = inv[3];
+        T dx = i00 * ex + i01 * ey;
+        T dy = i10 * ex + i11 * ey;
+        s.px = s.px - dx;
+        s.py = s.py - dy;
+        if (norm_below_1e6(dx * dx + dy * dy)) return true;  // :503, sqrt(.) < EPS
+        if (s.it == 99u) { s.st = ST_NUMERICAL_ERROR; return true; }  // :514
+        ++s.it;
+        return false;
+    }
+    // :520-524: (x, y, 1).normalize()
+    __device__ static __forceinline__ uint8_t newton_finish(const Newton& s, T& X, T& Y, T& Z) {
+        T n = sqrt(s.px * s.px + s.py * s.py + T(1) * T(1));
+        const T nq[2] = {s.px, s.py};
         T q[2];
         Z = div_shared(nq, n, q);  // X = px / n, Y = py / n, Z = 1 / n
         X = q[0];
         Y = q[1];
-        return st;
+        return s.st;
+    }
+    __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
+                                                        T& Z) {
+        Newton s;
+        if (!newton_init(c, u, v, s)) {
+            X = Y = Z = T(NAN);
+            return s.st;
+        }
+        while (!newton_step(c, s)) {
+        }
+        return newton_finish(s, X, Y, Z);
     }
 };
 
