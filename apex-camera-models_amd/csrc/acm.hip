@@ -76,8 +76,22 @@ static int dispatch_model(int model, F&& f) {
 // order (IEEE results: the host and a lane compute the same bits).
 template <class T>
 __host__ __device__ inline void unproject_consts(int model, const T* p, T* uk) {
-    uk[0] = uk[1] = T(0);
-    if (model == ACM_DOUBLE_SPHERE) {
+    uk[0] = uk[1] = uk[2] = uk[3] = T(0);
+    if (model == ACM_KANNALA_BRANDT) {
+        // uk[0]: 1 enables the certified fast Newton of
+        // KannalaBrandt::unproject, NaN disables it.  Its error bound assumes
+        // the polynomial's terms stay small on theta in [0, 2]:
+        // sum |k_i| 4^i <= 63 (other cameras take the reference loop).
+        const T b = T(4) * fabs(p[4]) + T(16) * fabs(p[5]) + T(64) * fabs(p[6]) +
+                    T(256) * fabs(p[7]);
+        uk[0] = b <= T(63) ? T(1) : T(NAN);
+    } else if (model == ACM_RADTAN) {
+        // uk[0]: the certified fast Newton of RadTan::unproject (1) or not
+        // (NaN); its error bound assumes |rad| <= 16 for |x|, |y| <= 2.
+        const T b = T(8) * fabs(p[4]) + T(64) * fabs(p[5]) + T(512) * fabs(p[8]) +
+                    T(16) * (fabs(p[6]) + fabs(p[7]));
+        uk[0] = b <= T(15) ? T(1) : T(NAN);
+    } else if (model == ACM_DOUBLE_SPHERE) {
         uk[0] = T(1) / (T(2) * p[4] - T(1));  // double_sphere.rs:205
     } else if (model == ACM_UCM) {
         const T gamma = T(1) - p[4];
@@ -92,7 +106,7 @@ __host__ __device__ inline void unproject_consts(int model, const T* p, T* uk) {
 // constants of Cam (prep): RN(1 / fx), RN(1 / fy) and unproject_consts.
 struct CamArg : acm_camera {
     double ifx, ify;
-    double uk[2];
+    double uk[4];
 };
 
 template <class T>
@@ -121,8 +135,8 @@ __device__ __forceinline__ Cam<T> make_cam(const CamArg& c) {
     k.hi = c.height;
     k.ifx = c.ifx;
     k.ify = c.ify;
-    k.uk[0] = c.uk[0];
-    k.uk[1] = c.uk[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) k.uk[i] = c.uk[i];
     return k;
 }
 
@@ -222,6 +236,7 @@ static std::atomic<int> g_sample_patience{-1};
 // RN(1 / fy) (div_by_f, bit-identical) instead of two IEEE divisions per
 // point: -1 = auto = on, 0 = off, 1 = on.
 static std::atomic<int> g_unproject_rcp{-1};
+static std::atomic<int> g_newton_fast{-1};
 // acm_lm_optimize without an all-reduce: the normal-equations epilogue writes
 // its P*P + P + 2 results straight into pinned host memory instead of device
 // memory + a device-to-host copy.  0 = off (copy + stream synchronise), 1 =
@@ -2245,6 +2260,8 @@ static CamArg prep(acm_camera c) {
     a.ifx = rcp ? recip(c.params[0]) : 0.0;
     a.ify = rcp ? recip(c.params[1]) : 0.0;
     unproject_consts<double>(c.model, c.params, a.uk);
+    if (g_newton_fast == 0 && (c.model == ACM_KANNALA_BRANDT || c.model == ACM_RADTAN))
+        a.uk[0] = NAN;  // fast Newton loops off
     return a;
 }
 
@@ -3074,6 +3091,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_SAMPLE_FUSED, &g_sample_fused, -1, 3, "value must be -1..3"},
         {ACM_TUNE_UNPROJECT_RCP, &g_unproject_rcp, -1, 1, "value must be -1..1"},
         {ACM_TUNE_SAMPLE_PATIENCE, &g_sample_patience, -1, 1 << 20, "value must be -1..2^20"},
+        {ACM_TUNE_NEWTON_FAST, &g_newton_fast, -1, 1, "value must be -1..1"},
     };
     for (const Knob& k : knobs) {
         if (k.key != key) continue;

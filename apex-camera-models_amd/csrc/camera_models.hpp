@@ -20,7 +20,15 @@
 //   * KB unproject: sin / cos of the Newton angle are polynomials on [0, 2]
 //     (sincos_0_2, OCML beyond), and after the Newton loop 1/ru and 1/|p|
 //     come from rcp_nr / rsq_nr (the IEEE forms outside [2^-1000, 2^1000]).
-//     The Newton iterates and every status decision are the reference's.
+//   * KB and RadTan unproject: the Newton loops are the certified fast ones
+//     (KannalaBrandt::newton_fast / front_fast, RadTan::newton_fast): FMA
+//     and reciprocal iterates (ru from rsq for KB, 1/|p| from rsq for
+//     RadTan) that make every break / continue / failure decision of the
+//     reference's loop, certified per step against an error bound; any
+//     pixel that cannot be certified runs the reference's loop from the
+//     start.  Statuses are the reference's; rays within a few ulp.
+//     ACM_TUNE_NEWTON_FAST = 0 runs the reference's loops for every pixel
+//     (RadTan's rays are then the reference's bit for bit).
 //   * FOV project: atan2 is atan2_ge0; FOV unproject: OCML sincos.
 //   * project<.., FAST = true> (the fused normal equations only): one
 //     reciprocal and products instead of the per-point divisions.
@@ -252,7 +260,7 @@ struct Cam {
     // instead), and uk = uniform subexpressions the reference evaluates per
     // point (IEEE results, identical wherever they are computed).
     T ifx, ify;
-    T uk[2];
+    T uk[4];
 };
 
 // (u - cx) / fx with fx uniform: RN(a / b) from the host's RN(1 / b) and the
@@ -410,6 +418,73 @@ struct RadTan {
         ++s.it;
         return false;
     }
+    // Certified fast Newton (double only), the RadTan analogue of
+    // KannalaBrandt::newton_fast.  The reference's step (:436-518) is ~110
+    // VALU instructions: unfused products and sums, j10 computed apart from
+    // j01 (they are equal), and four IEEE divisions by det.  Here the same
+    // step takes FMAs, j10 = j01 and 1 / det from v_rcp_f64 + one Newton
+    // step (~55 instructions).  Accepted only while |x|, |y| <= 2,
+    // |det| >= 1/16 and |j00| + |j11| + 2 |j01| <= 64 (so ||J^-1|| <= 1024)
+    // and both convergence tests (:459 on the error, :503 on the step) fall
+    // outside a 2^-10 relative band around the squared threshold; with the
+    // per-camera bound on the distortion terms (unproject_consts) the
+    // residual differs from the reference's by < 2e-14 and the step by
+    // < 2e-11, against a band of ~5e-10 on the norm.  Returns true only when
+    // the reference's loop breaks at the same step as converged (at most 12
+    // steps of its 100); anything uncertain, and every NaN, returns false and
+    // the caller runs newton_step from the start.
+    __device__ static __forceinline__ bool newton_fast(const Cam<T>& c, T tx, T ty, T& px,
+                                                       T& py) {
+        const T k1 = c.p[4], k2 = c.p[5], p1 = c.p[6], p2 = c.p[7], k3 = c.p[8];
+        const T k2d = k2 + k2, k3t = T(3) * k3, p1d = p1 + p1, p2d = p2 + p2;
+        const T p1s = T(6) * p1, p2s = T(6) * p2;
+        constexpr T lo = T(kNewtonTol2) * (T(1) - T(0x1p-10));
+        constexpr T hi = T(kNewtonTol2) * (T(1) + T(0x1p-10));
+        T x = tx, y = ty;
+        int state = 0;  // 0 iterating, 1 certified converged, 2 uncertain
+#pragma unroll 1
+        for (int i = 0; i < 12 && state == 0; ++i) {
+            const T x2 = x * x, y2 = y * y, xy = x * y;
+            const T s = x2 + y2;
+            const T rad = fma(fma(fma(k3, s, k2), s, k1), s, T(1));
+            const T xe = fma(x, rad, fma(p1d, xy, p2 * fma(x + x, x, s)));
+            const T ye = fma(y, rad, fma(p1, fma(y + y, y, s), p2d * xy));
+            const T ex = xe - tx, ey = ye - ty;
+            const T en2 = fma(ex, ex, ey * ey);
+            int st;
+            if (!(fabs(x) <= T(2) && fabs(y) <= T(2))) {
+                st = 2;
+            } else if (en2 < lo) {
+                st = 1;  // :459 breaks before the step
+            } else if (!(en2 > hi)) {
+                st = 2;  // in the band, or NaN
+            } else {
+                const T cm = fma(fma(k3t, s, k2d), s, k1);  // k1 + 2 k2 r2 + 3 k3 r4
+                const T w = cm + cm;
+                const T j00 = fma(x2, w, rad) + fma(p1d, y, p2s * x);
+                const T j11 = fma(y2, w, rad) + fma(p1s, y, p2d * x);
+                const T j01 = fma(xy, w, fma(p1d, x, p2d * y));
+                const T det = fma(j00, j11, -(j01 * j01));
+                const T sj = fabs(j00) + fabs(j11) + T(2) * fabs(j01);
+                if (!(fabs(det) >= T(0.0625) && sj <= T(64))) {
+                    st = 2;
+                } else {
+                    const T r0 = __builtin_amdgcn_rcp(det);
+                    const T id = fma(r0, fma(-det, r0, T(1)), r0);
+                    const T dx = fma(j11, ex, -(j01 * ey)) * id;
+                    const T dy = fma(j00, ey, -(j01 * ex)) * id;
+                    x -= dx;
+                    y -= dy;
+                    const T dn2 = fma(dx, dx, dy * dy);
+                    st = dn2 < lo ? 1 : (dn2 > hi ? 0 : 2);  // :503
+                }
+            }
+            state = st;
+        }
+        px = x;
+        py = y;
+        return state == 1;
+    }
     // :520-524: (x, y, 1).normalize()
     __device__ static __forceinline__ uint8_t newton_finish(const Newton& s, T& X, T& Y, T& Z) {
         T n = sqrt(s.px * s.px + s.py * s.py + T(1) * T(1));
@@ -427,6 +502,19 @@ struct RadTan {
             X = Y = Z = T(NAN);
             return s.st;
         }
+#ifndef ACM_IEEE_MATH
+        if constexpr (sizeof(T) == 8) {
+            T px, py;  // uk[0] NaN: unbounded terms, or ACM_TUNE_NEWTON_FAST = 0
+            if (c.uk[0] == c.uk[0] && newton_fast(c, s.tx, s.ty, px, py)) {
+                // (x, y, 1).normalize() with 1 / |p| from rsq + Newton (~1 ulp)
+                const T in = rsq_nr(fma(px, px, fma(py, py, T(1))));
+                X = px * in;
+                Y = py * in;
+                Z = in;
+                return ST_OK;
+            }
+        }
+#endif
         while (!newton_step(c, s)) {
         }
         return newton_finish(s, X, Y, Z);
@@ -500,6 +588,88 @@ struct KannalaBrandt {
         }
         return st;
     }
+    // Certified fast Newton (double only).  The reference's loop
+    // (kannala_brandt.rs:474-511) costs ~38 VALU instructions per step: the
+    // unfused products and sums it spells out plus an IEEE division.  Here
+    // each step is the same Newton step in Horner form with FMAs and
+    // delta = f * rcp(f') (~16 instructions), so the iterates differ from
+    // the reference's by rounding only.  The decisions are certified, not
+    // assumed: a step is accepted only when |f'| >= 1/16, |theta| <= 2 and
+    // |delta| lies outside [PREC (1 - 2^-12), PREC (1 + 2^-12)].  With the
+    // polynomial's terms bounded (sum |k_i| 4^i <= 63, checked per camera
+    // in unproject_consts; NaN coefficients otherwise) f differs from the
+    // reference's f by < 3e-13 and the iterates by < 4e-12, so the two
+    // deltas differ by < 1e-11, far inside the 2.4e-10 band: every accepted
+    // step makes the reference's break / continue decision, and the fast
+    // loop returns true only when it reached the reference's `break` within
+    // 6 steps (the reference gives up after 10).  Anything else -- a delta
+    // in the band, a small or non-finite f', a wandering theta, more than 6
+    // steps, NaN -- returns false and the caller runs the reference loop from
+    // the start, so the status is the reference's in every case and theta
+    // within a few ulp of its theta.
+    __device__ static __forceinline__ bool newton_fast(const Cam<T>& c, T ru, T& theta) {
+        const T k1 = c.p[4], k2 = c.p[5], k3 = c.p[6], k4 = c.p[7];
+        constexpr T lo = T(1e-6) * (T(1) - T(0x1p-12)), hi = T(1e-6) * (T(1) + T(0x1p-12));
+        // One lane state instead of early returns, and a rolled loop: an
+        // unrolled loop with per-lane exits kept one exec mask per exit live
+        // and spilled SGPRs in the sample_points tile loop.
+        T t = ru;
+        int state = 0;  // 0 iterating, 1 certified converged, 2 uncertain
+#pragma unroll 1
+        for (int i = 0; i < 6 && state == 0; ++i) {
+            // f = t P(s) - ru and f' = P(s) + 2 s P'(s), s = t^2, P(s) =
+            // 1 + k1 s + k2 s^2 + k3 s^3 + k4 s^4: P and P' by one Horner
+            // pass with synthetic division, so only k1..k4 are needed (the
+            // SGPR budget of the sample_points tile loop is tight)
+            const T s = t * t;
+            const T b3 = fma(k4, s, k3);
+            const T c2 = fma(k4, s, b3);
+            const T b2 = fma(b3, s, k2);
+            const T c1 = fma(c2, s, b2);
+            const T b1 = fma(b2, s, k1);
+            const T c0 = fma(c1, s, b1);
+            const T p = fma(b1, s, T(1));
+            const T fp = fma(s + s, c0, p);
+            const T f = fma(t, p, -ru);
+            // 1 / f' from v_rcp_f64 and one Newton step: relative error
+            // ~2^-44 at worst, i.e. < 1e-19 on a delta near the threshold
+            const T y0 = __builtin_amdgcn_rcp(fp);
+            const T y = fma(y0, fma(-fp, y0, T(1)), y0);
+            const T d = f * y;
+            t -= d;
+            const T ad = fabs(d);
+            // |f'| <= 1 + 9 * 63 here (|t| <= 2, bounded terms): only the
+            // lower bound (and NaN) needs a test
+            const bool sane = fabs(fp) >= T(0.0625) && fabs(t) <= T(2);
+            state = !sane ? 2 : (ad < lo ? 1 : (ad > hi ? 0 : 2));  // band or NaN: 2
+        }
+        theta = t;
+        return state == 1;
+    }
+    // The front of the unprojection on the certified path: ru from rsq + two
+    // Newton steps (within ~1 ulp of the reference's IEEE sqrt, which is
+    // within the Newton loop's error budget above) with the reference's two
+    // decisions on it certified the same way -- ru > 1e-6 (:472) and the
+    // pi/2 clamp (:467) are taken only when ru is 2^-30 (relative) away from
+    // either threshold -- then newton_fast.  Returns false when anything is
+    // uncertain; the caller then runs the reference's own sequence.  On
+    // success ir ~= 1 / ru (the rsq itself, or 2 / pi after the clamp).
+    __device__ static __forceinline__ bool front_fast(const Cam<T>& c, T r2, T& ru, T& theta,
+                                                      T& ir) {
+        // uk[0] NaN: the camera's terms are unbounded, or ACM_TUNE_NEWTON_FAST = 0
+        if (!nr_range(r2) || !(c.uk[0] == c.uk[0])) return false;
+        const T y = rsq_nr(r2);
+        const T rf = r2 * y;
+        constexpr T kHalfPi = T(kPi / 2.0);
+        constexpr T kLoPrec = T(1e-6) * (T(1) + T(0x1p-30));
+        constexpr T kClampLo = kHalfPi * (T(1) - T(0x1p-30)), kClampHi = kHalfPi * (T(1) + T(0x1p-30));
+        if (!(rf > kLoPrec)) return false;
+        const bool clamp = rf > kClampHi;
+        if (!clamp && !(rf < kClampLo)) return false;
+        ru = clamp ? kHalfPi : rf;
+        ir = clamp ? T(2.0 / kPi) : y;
+        return newton_fast(c, ru, theta);
+    }
     // kannala_brandt.rs:445-562: Newton on theta_d(theta) = ru, <=10 steps.
     __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
                                                         T& Z) {
@@ -511,29 +681,37 @@ struct KannalaBrandt {
         }
         T mx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
         T my = div_by_f(v - cy, fy, c.ify);
-        T ru = sqrt(mx * mx + my * my);
-        ru = fmin(ru, T(kPi / 2.0));  // :467, f64::min semantics
-        T theta = ru;
+        const T r2 = mx * mx + my * my;
         const T PREC = T(1e-6);
+        T ru, theta, ir_fast = T(0);
         bool converged = true;
-        if (ru > PREC) {
-            for (int i = 0; i < 10; ++i) {
-                T theta2 = theta * theta;
-                T theta4 = theta2 * theta2;
-                T theta6 = theta4 * theta2;
-                T theta8 = theta4 * theta4;
-                T k1t2 = k1 * theta2, k2t4 = k2 * theta4, k3t6 = k3 * theta6, k4t8 = k4 * theta8;
-                T f = theta * (T(1) + k1t2 + k2t4 + k3t6 + k4t8) - ru;
-                T fp = T(1) + (T(3) * k1t2) + (T(5) * k2t4) + (T(7) * k3t6) + (T(9) * k4t8);
-                if (fabs(fp) < T(kEps)) { converged = false; break; }
-                T delta = f / fp;
-                theta -= delta;
-                if (fabs(delta) < PREC) break;
-                if (i == 9) converged = false;
+        bool certified = false;
+#ifndef ACM_IEEE_MATH
+        if constexpr (sizeof(T) == 8) certified = front_fast(c, r2, ru, theta, ir_fast);
+#endif
+        if (!certified) {  // the reference's sequence (:462-525)
+            ru = sqrt(r2);
+            ru = fmin(ru, T(kPi / 2.0));  // :467, f64::min semantics
+            theta = ru;
+            if (ru > PREC) {
+                for (int i = 0; i < 10; ++i) {
+                    T theta2 = theta * theta;
+                    T theta4 = theta2 * theta2;
+                    T theta6 = theta4 * theta2;
+                    T theta8 = theta4 * theta4;
+                    T k1t2 = k1 * theta2, k2t4 = k2 * theta4, k3t6 = k3 * theta6, k4t8 = k4 * theta8;
+                    T f = theta * (T(1) + k1t2 + k2t4 + k3t6 + k4t8) - ru;
+                    T fp = T(1) + (T(3) * k1t2) + (T(5) * k2t4) + (T(7) * k3t6) + (T(9) * k4t8);
+                    if (fabs(fp) < T(kEps)) { converged = false; break; }
+                    T delta = f / fp;
+                    theta -= delta;
+                    if (fabs(delta) < PREC) break;
+                    if (i == 9) converged = false;
+                }
+            } else {
+                if (ru > T(0)) converged = false;
+                else { theta = T(0); }
             }
-        } else {
-            if (ru > T(0)) converged = false;
-            else { theta = T(0); }
         }
         const bool small = fabs(ru) < T(kEps);
         T s, co;
@@ -544,7 +722,7 @@ struct KannalaBrandt {
             // decision depends on it, and the ray is held to 1e-10 anyway
             // (sin / cos are polynomials).  1 / ru and 1 / |p| from rcp / rsq
             // + Newton (~1 ulp) instead of two IEEE divisions and a sqrt.
-            const T ir = nr_range(ru) ? rcp_nr(ru) : T(1) / ru;
+            const T ir = certified ? ir_fast : (nr_range(ru) ? rcp_nr(ru) : T(1) / ru);
             const T xc = small ? T(0) : mx * ir;  // mx / ru
             const T yc = small ? T(0) : my * ir;
             const T px = s * xc, py = s * yc;

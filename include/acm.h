@@ -413,6 +413,13 @@ ACM_API int acm_stream_synchronize(void *stream);
  * spends on a predecessor tile that has not published its count before the
  * waiting wave counts that tile's cells itself (-1 = auto = 512; 0 = at once,
  * which exercises that path; outputs are identical for every value).
+ * ACM_TUNE_NEWTON_FAST: the certified fast Newton loops of the KB and RadTan
+ * unprojections (acm_unproject, acm_sample_points*; camera_models.hpp
+ * newton_fast): FMA / reciprocal iterates whose every break / continue
+ * decision is certified against the reference's, with the reference's own
+ * loop for any pixel that cannot be certified (-1 = auto = on, 0 = the
+ * reference's loop for every pixel, 1 = on).  Statuses are identical for
+ * every value; rays agree within a few ulp.
  * Every knob is an atomic: acm_set_tuning may race with any other call.
  * Returns the previous value or an error. */
 enum {
@@ -427,7 +434,8 @@ enum {
     ACM_TUNE_LM_HOST_RESULT = 8,
     ACM_TUNE_SAMPLE_FUSED = 9,
     ACM_TUNE_UNPROJECT_RCP = 10,
-    ACM_TUNE_SAMPLE_PATIENCE = 11
+    ACM_TUNE_SAMPLE_PATIENCE = 11,
+    ACM_TUNE_NEWTON_FAST = 12
 };
 ACM_API int acm_set_tuning(int key, int value);
 

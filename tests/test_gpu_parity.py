@@ -25,6 +25,33 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-10
 NO_TRANSCENDENTAL_PROJECT = (0, 1, 3, 4, 5)
 NO_TRANSCENDENTAL_UNPROJECT = (0, 1, 3, 4, 5)
+# Models whose default unprojection returns the reference's rays bit for bit.
+# RadTan's (and KB's) default Newton loop is the certified fast one
+# (ACM_TUNE_NEWTON_FAST): statuses exact, rays within a few ulp;
+# test_newton_reference_loop_bit_exact pins the knob-off path bit for bit.
+EXACT_RAYS_UNPROJECT = (0, 3, 4, 5)
+ULP = 2.0 ** -52
+
+
+def ulps_of_one(a, b):
+    """max |a - b| in units of ulp(1) over finite entries (unit rays)"""
+    fin = np.isfinite(b)
+    assert np.array_equal(fin, np.isfinite(a)), "finite pattern differs"
+    return float(np.abs(a[fin] - b[fin]).max() / ULP) if fin.any() else 0.0
+
+
+class newton_fast:
+    """with newton_fast(0): the reference's Newton loops for every pixel"""
+    def __init__(self, value):
+        self.value = value
+
+    def __enter__(self):
+        from apex_camera_models import _lib
+        _lib.load().acm_set_tuning(_lib.TUNE_NEWTON_FAST, self.value)
+
+    def __exit__(self, *exc):
+        from apex_camera_models import _lib
+        _lib.load().acm_set_tuning(_lib.TUNE_NEWTON_FAST, -1)
 
 
 @pytest.fixture(scope="module")
@@ -87,8 +114,74 @@ def test_unproject_vs_golden(be, golden_dir, model, layout):
     rays, st = be.unproject(model, params, w, h, g["uv_in"], layout=layout)
     assert np.array_equal(st, g["unproj_status"]), np.nonzero(st != g["unproj_status"])
     assert rel_err(rays, g["rays"], floor=1.0) <= TOL
-    if model in NO_TRANSCENDENTAL_UNPROJECT:
+    if model in EXACT_RAYS_UNPROJECT:
         assert np.array_equal(rays, g["rays"], equal_nan=True)
+    if model == 1:
+        assert ulps_of_one(rays[st == 0], g["rays"][st == 0]) <= 8
+
+
+@pytest.mark.parametrize("model", [1, 2])
+def test_newton_reference_loop_bit_exact(be, golden_dir, model):
+    """ACM_TUNE_NEWTON_FAST = 0 runs the reference's own Newton loop for
+    every pixel: RadTan rays then equal the golden (oracle) rays bit for bit,
+    in acm_unproject and in sample_points; KB's stay within 1e-10 (its sin /
+    cos are polynomials either way).  Statuses are the same in both modes."""
+    from apex_camera_models import util
+    from test_oracle import SAMPLES
+    g, params, w, h = _golden(golden_dir, model)
+    with newton_fast(0):
+        rays, st = be.unproject(model, params, w, h, g["uv_in"])
+    assert np.array_equal(st, g["unproj_status"])
+    if model == 1:
+        assert np.array_equal(rays, g["rays"], equal_nan=True)
+    else:
+        assert rel_err(rays, g["rays"], floor=1.0) <= TOL
+    sp, (sw, sh) = SAMPLES[model]
+    m = _model_obj(model, sp, sw, sh)
+    uv0, xyz0, _ = O.sample_points(model, sp, sw, sh, 20_000)
+    with newton_fast(0):
+        uv, xyz = util.sample_points(m, 20_000)
+    assert np.array_equal(uv.cpu().numpy(), uv0)
+    if model == 1:
+        assert np.array_equal(xyz.cpu().numpy(), xyz0)
+
+
+# strongly distorted cameras inside the fast loops' per-camera bounds (and one
+# RadTan camera outside them), as in tools/diag_newton_fast.py
+NEWTON_STRESS = [
+    (2, [190.97847715128717, 190.9733070521226, 254.93170605935475, 256.8974428996504,
+         0.5, -0.3, 0.1, -0.02], (512, 512)),
+    (2, [190.97847715128717, 190.9733070521226, 254.93170605935475, 256.8974428996504,
+         -0.2, 0.15, -0.05, 0.004], (512, 512)),
+    (1, [461.629, 460.152, 362.680, 246.049, -0.45, 0.12, 0.003, -0.002, -0.005], (752, 480)),
+    (1, [461.629, 460.152, 362.680, 246.049, 0.3, -0.05, 0.01, 0.01, 0.002], (752, 480)),
+    (1, [461.629, 460.152, 362.680, 246.049, -0.6, 0.45, 0.003, -0.002, -0.1], (752, 480)),
+]
+
+
+@pytest.mark.parametrize("case", range(len(NEWTON_STRESS)))
+def test_newton_fast_statuses_identical_under_stress(be, case):
+    """The certified fast loops against the reference's loop on 1M pixels
+    spread over the image and a 10-pixel margin of strongly distorted
+    cameras, where Newton fails for up to 20% of the pixels and many deltas
+    pass near the threshold: identical statuses (the certificate's claim),
+    and rays within 32 ulp of 1 (KB's third stress camera reaches ~24: its
+    Newton steps amplify rounding), against the oracle too."""
+    model, params, (w, h) = NEWTON_STRESS[case]
+    rng = np.random.default_rng(case)
+    n = 1_000_000
+    px = np.stack([rng.uniform(-10, w + 10, n), rng.uniform(-10, h + 10, n)], 1)
+    rays1, st1 = be.unproject(model, params, w, h, px)
+    with newton_fast(0):
+        rays0, st0 = be.unproject(model, params, w, h, px)
+    assert np.array_equal(st1, st0), np.nonzero(st1 != st0)[0][:5]
+    ok = st0 == 0
+    assert ulps_of_one(rays1[ok], rays0[ok]) <= 32
+    sub = slice(0, 50_000)
+    r_o, s_o = O.unproject(model, params, w, h, px[sub])
+    assert np.array_equal(st1[sub], s_o)
+    if model == 1:
+        assert np.array_equal(rays0[sub][s_o == 0], r_o[s_o == 0], equal_nan=True)
 
 
 @pytest.mark.parametrize("case", kat_suite.ALL, ids=lambda f: f.__name__)
@@ -272,7 +365,7 @@ def test_sample_points_vs_oracle(model, n):
     assert uv.shape[0] == uv0.shape[0]  # same kept set ...
     assert np.array_equal(uv.cpu().numpy(), uv0)  # ... in the same order, bit-exact pixels
     assert rel_err(xyz.cpu().numpy(), xyz0, floor=1.0) <= TOL
-    if model in NO_TRANSCENDENTAL_UNPROJECT:
+    if model in EXACT_RAYS_UNPROJECT:
         assert np.array_equal(xyz.cpu().numpy(), xyz0)
 
 
@@ -299,7 +392,7 @@ def test_sample_points_every_path_matches_oracle(model):
             uv, xyz = util.sample_points(m, n)
             assert np.array_equal(uv.cpu().numpy(), uv0), v
             assert rel_err(xyz.cpu().numpy(), xyz0, floor=1.0) <= TOL, v
-            if model in NO_TRANSCENDENTAL_UNPROJECT:
+            if model in EXACT_RAYS_UNPROJECT:
                 assert np.array_equal(xyz.cpu().numpy(), xyz0), v
             fn = gpu_sample_points_range(m, n)
             parts = [fn(*grid_row_range(ncx, ncy, r, 3)) for r in range(3)]
@@ -519,7 +612,8 @@ def test_status_on_thresholds_matches_oracle(be):
     """tests/boundary_probes.py: +-8 ulps around every threshold root; the
     kernels' statuses equal the oracle's (which test_boundaries.py pins to a
     binary64 emulation of the Rust conditions), values bit-exact for the
-    models without a transcendental and within 1e-10 for KB."""
+    models without a transcendental (RadTan's unprojection within 8 ulp: its
+    default Newton loop is the certified fast one) and within 1e-10 for KB."""
     import boundary_probes as B
     for model, p, (w, h), kind, pts in B.probes():
         if kind == "project":
@@ -532,5 +626,7 @@ def test_status_on_thresholds_matches_oracle(be):
         ok = st0 == 0
         if model == 2:
             assert rel_err(uv[ok], uv0[ok], floor=1.0) <= TOL
+        elif model == 1 and kind == "unproject":  # the certified fast Newton
+            assert ulps_of_one(uv[ok], uv0[ok]) <= 8
         else:
             assert np.array_equal(uv[ok], uv0[ok], equal_nan=True), (model, kind)
