@@ -68,6 +68,7 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
 TUNE_PROJECT_VARIANT, TUNE_RESIDUAL_NT, TUNE_NE_WAVES, TUNE_FOV_UNROLL, TUNE_NE_UNROLL = 0, 1, 2, 3, 4
 TUNE_ALIGN_J, TUNE_NT_LOADS, TUNE_NT_LOADS_UNPROJECT, TUNE_LM_HOST_RESULT = 5, 6, 7, 8
 TUNE_SAMPLE_FUSED, TUNE_UNPROJECT_RCP, TUNE_SAMPLE_PATIENCE, TUNE_NEWTON_FAST = 9, 10, 11, 12
+TUNE_UNPROJECT_PPT = 13
 ERR_NOT_SUPPORTED = -6
 ERR_NUMERICAL = -7
 LM_TERMINATION = {0: "MaxIterations", 1: "CostTolerance", 2: "ParameterTolerance",

@@ -237,6 +237,7 @@ static std::atomic<int> g_sample_patience{-1};
 // point: -1 = auto = on, 0 = off, 1 = on.
 static std::atomic<int> g_unproject_rcp{-1};
 static std::atomic<int> g_newton_fast{-1};
+static std::atomic<int> g_unproject_ppt{-1};
 // acm_lm_optimize without an all-reduce: the normal-equations epilogue writes
 // its P*P + P + 2 results straight into pinned host memory instead of device
 // memory + a device-to-host copy.  0 = off (copy + stream synchronise), 1 =
@@ -495,30 +496,78 @@ __device__ __forceinline__ void st1d(double* p, double v) {
     else *p = v;
 }
 
-template <class TagT, int LAYOUT, bool NT, bool NTL>
+// PPT pixels per lane: a workgroup owns PPT x 256 consecutive pixels, round
+// r of lane t is pixel 256 r + t (every load and store instruction stays
+// fully coalesced) and all PPT loads are issued before the first
+// unprojection.  With one pixel per lane a 10M-pixel launch is 39K
+// workgroups that each move only 10.5 KB: the closed-form models ran at the
+// workgroup dispatch rate (~1.8 ns per workgroup, 5.7 TB/s for Pinhole).
+// STG (AoS, rays 16-B aligned): a wave's 64 rays are 1536 contiguous bytes;
+// they are staged in LDS and written as 96 16-B pieces (two store
+// instructions per wave, every lane's address 16 B after its neighbour's)
+// instead of three 8-B stores per lane at a 24-B stride.
+template <class TagT, int LAYOUT, bool NT, bool NTL, int PPT, bool STG>
 __global__ __launch_bounds__(kBlock) void k_unproject(CamArg cam, size_t n,
                                                       const double* __restrict__ uv,
                                                       double* __restrict__ rays,
                                                       uint8_t* __restrict__ status) {
     using M = typename TagT::template type<double>;
-    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
+    const size_t i0 = (size_t)blockIdx.x * (kBlock * PPT) + threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const Cam<double> c = make_cam<double>(cam);
-    const double2 q = ld2<NTL>(uv + 2 * i);
-    double X, Y, Z;
-    const uint8_t st = M::unproject(c, q.x, q.y, X, Y, Z);
-    if (st != ST_OK) X = Y = Z = __builtin_nan("");
-    if (LAYOUT == ACM_LAYOUT_AOS) {
-        st1d<NT>(rays + 3 * i, X);
-        st1d<NT>(rays + 3 * i + 1, Y);
-        st1d<NT>(rays + 3 * i + 2, Z);
-    } else {
-        st1d<NT>(rays + i, X);
-        st1d<NT>(rays + n + i, Y);
-        st1d<NT>(rays + 2 * n + i, Z);
+    __shared__ double s_ray[STG ? kBlock / 64 : 1][STG ? 64 * 3 : 1];
+    double2 q[PPT];
+#pragma unroll
+    for (int r = 0; r < PPT; ++r) {
+        const size_t i = i0 + (size_t)r * kBlock;
+        q[r] = i < n ? ld2<NTL>(uv + 2 * i) : double2{0.0, 0.0};
     }
-    st1<NT>(status + i, st);
+#pragma unroll
+    for (int r = 0; r < PPT; ++r) {
+        const size_t i = i0 + (size_t)r * kBlock;
+        const size_t wfirst = i - (size_t)lane;  // the wave's first pixel this round
+        if (wfirst >= n) break;                  // wave-uniform
+        double X = 0.0, Y = 0.0, Z = 0.0;
+        uint8_t st = ST_OK;
+        if (i < n) {
+            st = M::unproject(c, q[r].x, q[r].y, X, Y, Z);
+            if (st != ST_OK) X = Y = Z = __builtin_nan("");
+        }
+        if (LAYOUT == ACM_LAYOUT_AOS) {
+            if (STG && wfirst + 64 <= n) {  // whole wave in range
+                double* sr = s_ray[STG ? wid : 0];
+                sr[3 * lane] = X;
+                sr[3 * lane + 1] = Y;
+                sr[3 * lane + 2] = Z;
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                double* dst = rays + 3 * wfirst;
+                st2<NT>(dst + 2 * lane, sr[2 * lane], sr[2 * lane + 1]);
+                if (lane < 32) st2<NT>(dst + 128 + 2 * lane, sr[128 + 2 * lane], sr[129 + 2 * lane]);
+                __builtin_amdgcn_wave_barrier();  // the next round rewrites sr
+            } else if (i < n) {
+                st1d<NT>(rays + 3 * i, X);
+                st1d<NT>(rays + 3 * i + 1, Y);
+                st1d<NT>(rays + 3 * i + 2, Z);
+            }
+        } else if (i < n) {
+            st1d<NT>(rays + i, X);
+            st1d<NT>(rays + n + i, Y);
+            st1d<NT>(rays + 2 * n + i, Z);
+        }
+        if (i < n) st1<NT>(status + i, st);
+    }
 }
+
+// LDS-staged AoS ray stores by default for the models whose unprojection is
+// memory-bound (Pinhole, DS, UCM, EUCM: 6.0-6.4 -> 6.4-7.2 TB/s at 10M
+// pixels); the VALU-bound ones (KB, RadTan, FOV) lose 4-6% to the extra LDS
+// and wave-barrier work (profiles/r02e_unproject_ppt.log).
+template <class TagT> struct UnprojectStaged { static constexpr bool on = true; };
+template <> struct UnprojectStaged<Tag<KannalaBrandt>> { static constexpr bool on = false; };
+template <> struct UnprojectStaged<Tag<RadTan>> { static constexpr bool on = false; };
+template <> struct UnprojectStaged<Tag<Fov>> { static constexpr bool on = false; };
 
 #ifdef ACM_DIAG_REFILL
 // Diagnostic build (ACM_DIAG_REFILL = K): RadTan acm_unproject with lane
@@ -2490,11 +2539,29 @@ ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_
             return check_launch("acm_unproject");
         }
 #endif
+        // knob: -1 auto = 2 pixels per lane, AoS stores LDS-staged per
+        // UnprojectStaged; 1 / 2 = pixels per lane with three 8-B stores per
+        // AoS ray; 3 = 1 pixel per lane with LDS-staged stores
+        // (tools/diag_unproject_ppt.py)
+        const int ppt = g_unproject_ppt;
+        const bool stg = (ppt == 3 || (ppt < 0 && UnprojectStaged<TagT>::on)) &&
+                         (reinterpret_cast<uintptr_t>(rays) & 15u) == 0;
         auto go = [&](auto lay_c) {
             constexpr int L = decltype(lay_c)::value;
-            auto kern = nt ? (ntl ? k_unproject<TagT, L, true, true> : k_unproject<TagT, L, true, false>)
-                           : (ntl ? k_unproject<TagT, L, false, true> : k_unproject<TagT, L, false, false>);
-            hipLaunchKernelGGL(kern, g, b, 0, s, prep(*cam), n, points_2d, rays, status);
+            auto pick = [&](auto ppt_c, auto stg_c) {
+                constexpr int K = decltype(ppt_c)::value;
+                constexpr bool PR = decltype(stg_c)::value && L == ACM_LAYOUT_AOS;
+                auto kern = nt ? (ntl ? k_unproject<TagT, L, true, true, K, PR> : k_unproject<TagT, L, true, false, K, PR>)
+                               : (ntl ? k_unproject<TagT, L, false, true, K, PR> : k_unproject<TagT, L, false, false, K, PR>);
+                const dim3 gk((unsigned)((n + (size_t)kBlock * K - 1) / ((size_t)kBlock * K)));
+                hipLaunchKernelGGL(kern, gk, b, 0, s, prep(*cam), n, points_2d, rays, status);
+            };
+            using One = std::integral_constant<int, 1>;
+            using Two = std::integral_constant<int, 2>;
+            if (ppt == 1) pick(One{}, std::false_type{});
+            else if (ppt == 3) pick(One{}, std::true_type{});
+            else if (stg) pick(Two{}, std::true_type{});
+            else pick(Two{}, std::false_type{});
         };
         if (layout == ACM_LAYOUT_AOS) go(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else go(std::integral_constant<int, ACM_LAYOUT_SOA>{});
@@ -3092,12 +3159,14 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_UNPROJECT_RCP, &g_unproject_rcp, -1, 1, "value must be -1..1"},
         {ACM_TUNE_SAMPLE_PATIENCE, &g_sample_patience, -1, 1 << 20, "value must be -1..2^20"},
         {ACM_TUNE_NEWTON_FAST, &g_newton_fast, -1, 1, "value must be -1..1"},
+        {ACM_TUNE_UNPROJECT_PPT, &g_unproject_ppt, -1, 3, "value must be -1..3"},
     };
     for (const Knob& k : knobs) {
         if (k.key != key) continue;
         bool ok = value >= k.lo && value <= k.hi;
         if (key == ACM_TUNE_NE_WAVES) ok = ok && value != 2;
         if (key == ACM_TUNE_FOV_UNROLL) ok = ok && value != 3;
+        if (key == ACM_TUNE_UNPROJECT_PPT) ok = ok && value != 0;
         if (!ok) return fail(ACM_ERR_INVALID_ARGUMENT, k.msg);
         return k.v->exchange(value);
     }

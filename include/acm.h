@@ -420,6 +420,12 @@ ACM_API int acm_stream_synchronize(void *stream);
  * loop for any pixel that cannot be certified (-1 = auto = on, 0 = the
  * reference's loop for every pixel, 1 = on).  Statuses are identical for
  * every value; rays agree within a few ulp.
+ * ACM_TUNE_UNPROJECT_PPT: acm_unproject's pixels per lane and AoS ray
+ * stores (-1 = auto = 2 pixels per lane; for Pinhole, DS, UCM and EUCM each
+ * wave's 64 AoS rays staged in LDS and written as 16-B pieces when rays is
+ * 16-B aligned; 1 / 2 = pixels per lane with three 8-B stores per ray; 3 =
+ * 1 pixel per lane, staged).
+ * Outputs are identical for every value.
  * Every knob is an atomic: acm_set_tuning may race with any other call.
  * Returns the previous value or an error. */
 enum {
@@ -435,7 +441,8 @@ enum {
     ACM_TUNE_SAMPLE_FUSED = 9,
     ACM_TUNE_UNPROJECT_RCP = 10,
     ACM_TUNE_SAMPLE_PATIENCE = 11,
-    ACM_TUNE_NEWTON_FAST = 12
+    ACM_TUNE_NEWTON_FAST = 12,
+    ACM_TUNE_UNPROJECT_PPT = 13
 };
 ACM_API int acm_set_tuning(int key, int value);
 

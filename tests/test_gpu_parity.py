@@ -630,3 +630,41 @@ def test_status_on_thresholds_matches_oracle(be):
             assert ulps_of_one(uv[ok], uv0[ok]) <= 8
         else:
             assert np.array_equal(uv[ok], uv0[ok], equal_nan=True), (model, kind)
+
+
+@pytest.mark.parametrize("n", [1, 255, 257, 1000, 65537])
+def test_unproject_every_store_form_identical(n):
+    """ACM_TUNE_UNPROJECT_PPT: 1 or 2 pixels per lane, three 8-B stores per
+    AoS ray or a wave's rays staged in LDS and written as 16-B pieces, on
+    ragged sizes and with the ray buffer 16-B aligned or only 8-B aligned
+    (staging then falls back): every form writes the same bytes."""
+    import ctypes
+    import torch
+    from apex_camera_models import _lib, samples
+    L = _lib.load()
+    rng = np.random.default_rng(n)
+    for model in (0, 1, 2):
+        params, (w, h) = samples.SAMPLES[model]
+        cam = _lib.AcmCamera()
+        _lib.check(L.acm_camera_init(ctypes.byref(cam), model,
+                                     (ctypes.c_double * len(params))(*params), len(params), w, h))
+        px = torch.as_tensor(np.stack([rng.uniform(-5, w + 5, n), rng.uniform(-5, h + 5, n)], 1),
+                             device="cuda")
+        outs = []
+        try:
+            for v in (-1, 1, 2, 3):
+                L.acm_set_tuning(_lib.TUNE_UNPROJECT_PPT, v)
+                for shift in (0, 1):  # rays at +0 or +8 bytes
+                    buf = torch.full((3 * n + 2,), 7.0, dtype=torch.float64, device="cuda")
+                    st = torch.full((n,), 9, dtype=torch.uint8, device="cuda")
+                    _lib.check(L.acm_unproject(ctypes.byref(cam), n, px.data_ptr(),
+                                               buf[shift:].data_ptr(), 0, st.data_ptr(), None))
+                    torch.cuda.synchronize()
+                    b = buf.cpu().numpy()
+                    assert b[0] == 7.0 or shift == 0
+                    assert b[3 * n + shift:].tolist() == [7.0] * (2 - shift)  # nothing past the end
+                    outs.append((b[shift:shift + 3 * n].view(np.int64), st.cpu().numpy()))
+        finally:
+            L.acm_set_tuning(_lib.TUNE_UNPROJECT_PPT, -1)
+        for r, s in outs[1:]:
+            assert np.array_equal(r, outs[0][0]) and np.array_equal(s, outs[0][1]), model
