@@ -91,6 +91,11 @@ __host__ __device__ inline void unproject_consts(int model, const T* p, T* uk) {
         const T b = T(8) * fabs(p[4]) + T(64) * fabs(p[5]) + T(512) * fabs(p[8]) +
                     T(16) * (fabs(p[6]) + fabs(p[7]));
         uk[0] = b <= T(15) ? T(1) : T(NAN);
+    } else if (model == ACM_FOV) {
+        // Fov::unproject's fast form: uk[0] = 1 (NaN: off), uk[1] =
+        // 1 / (2 tan(w / 2)) (p[8] = tan(w / 2), set by prep on the host)
+        uk[0] = T(1);
+        uk[1] = T(1) / (T(2) * p[8]);
     } else if (model == ACM_DOUBLE_SPHERE) {
         uk[0] = T(1) / (T(2) * p[4] - T(1));  // double_sphere.rs:205
     } else if (model == ACM_UCM) {
@@ -561,13 +566,12 @@ __global__ __launch_bounds__(kBlock) void k_unproject(CamArg cam, size_t n,
 }
 
 // LDS-staged AoS ray stores by default for the models whose unprojection is
-// memory-bound (Pinhole, DS, UCM, EUCM: 6.0-6.4 -> 6.4-7.2 TB/s at 10M
-// pixels); the VALU-bound ones (KB, RadTan, FOV) lose 4-6% to the extra LDS
-// and wave-barrier work (profiles/r02e_unproject_ppt.log).
+// memory-bound (Pinhole, DS, UCM, EUCM, FOV: 6.0-6.4 -> 6.4-7.2 TB/s at 10M
+// pixels); the VALU-bound ones (KB, RadTan) lose 4-6% to the extra LDS and
+// wave-barrier work (profiles/r02e_unproject_ppt.log).
 template <class TagT> struct UnprojectStaged { static constexpr bool on = true; };
 template <> struct UnprojectStaged<Tag<KannalaBrandt>> { static constexpr bool on = false; };
 template <> struct UnprojectStaged<Tag<RadTan>> { static constexpr bool on = false; };
-template <> struct UnprojectStaged<Tag<Fov>> { static constexpr bool on = false; };
 
 #ifdef ACM_DIAG_REFILL
 // Diagnostic build (ACM_DIAG_REFILL = K): RadTan acm_unproject with lane
@@ -1371,6 +1375,9 @@ template <class TagT> struct SampleR { static constexpr int R = 4; };
 // profiles/r02_diag_sample.log, r02b_diag_sample.log).
 template <class TagT> struct SampleSinglePass { static constexpr bool on = true; };
 template <> struct SampleSinglePass<Tag<Pinhole>> { static constexpr bool on = false; };
+// FOV's unprojection became cheap with its reciprocal form (r02e): two-pass
+// 1.04 vs single pass 1.15 ms at 1e8 cells (profiles/r02e_diag_sample.log).
+template <> struct SampleSinglePass<Tag<Fov>> { static constexpr bool on = false; };
 constexpr size_t kFusedCells = (size_t)kBlock * kFusedRMin;
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
 constexpr int kLbPatience = 512;  // polls (s_sleep between) before computing a count itself
@@ -2309,8 +2316,9 @@ static CamArg prep(acm_camera c) {
     a.ifx = rcp ? recip(c.params[0]) : 0.0;
     a.ify = rcp ? recip(c.params[1]) : 0.0;
     unproject_consts<double>(c.model, c.params, a.uk);
-    if (g_newton_fast == 0 && (c.model == ACM_KANNALA_BRANDT || c.model == ACM_RADTAN))
-        a.uk[0] = NAN;  // fast Newton loops off
+    if (g_newton_fast == 0 &&
+        (c.model == ACM_KANNALA_BRANDT || c.model == ACM_RADTAN || c.model == ACM_FOV))
+        a.uk[0] = NAN;  // fast Newton loops / FOV fast unprojection off
     return a;
 }
 
@@ -2833,8 +2841,8 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
     // (plain stores: non-temporal ones measured slower for these compacted
     // outputs, 1.41 -> 1.47 ms at 1e8 KB cells, profiles/r02_diag_sample_phases.log)
     int fused = g_sample_fused;
-    if (fused < 0 && cam->model == ACM_PINHOLE &&
-        !SampleSinglePass<Tag<Pinhole>>::on)
+    if (fused < 0 && ((cam->model == ACM_PINHOLE && !SampleSinglePass<Tag<Pinhole>>::on) ||
+                      (cam->model == ACM_FOV && !SampleSinglePass<Tag<Fov>>::on)))
         fused = 0;
     if (fused != 0) {
         uint64_t* status = (uint64_t*)workspace + 1;

@@ -29,7 +29,9 @@
 //     start.  Statuses are the reference's; rays within a few ulp.
 //     ACM_TUNE_NEWTON_FAST = 0 runs the reference's loops for every pixel
 //     (RadTan's rays are then the reference's bit for bit).
-//   * FOV project: atan2 is atan2_ge0; FOV unproject: OCML sincos.
+//   * FOV project: atan2 is atan2_ge0; FOV unproject: sincos_0_2 and
+//     rsq / rcp + Newton for 1 / rd, 1 / cos and 1 / |p| (its one decision,
+//     rd > sqrt(EPS), taken exactly on r2).
 //   * project<.., FAST = true> (the fused normal equations only): one
 //     reciprocal and products instead of the per-point divisions.
 // None of these feeds a status decision, so statuses are bit-exact
@@ -969,6 +971,35 @@ struct Fov {
         T mul2 = tan_w_2 * T(2);
         T mx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
         T my = div_by_f(v - cy, fy, c.ify);
+#ifndef ACM_IEEE_MATH
+        if constexpr (sizeof(T) == 8) {
+            // Values-only fast form (uk[0] == 1; ACM_TUNE_NEWTON_FAST = 0 sets
+            // NaN): rd and 1 / rd from rsq, sin / cos of rd w by sincos_0_2,
+            // 1 / cos and 1 / |p| by rcp / rsq + Newton (~1-2 ulp each).  The
+            // one decision, rd > sqrt(EPS) = 2^-26 (:320), is taken on r2
+            // exactly: RN(sqrt(r2)) > 2^-26  <=>  r2 > 2^-52 (1 + 2^-52).
+            const T r2 = mx * mx + my * my;
+            if (c.uk[0] == c.uk[0] && r2 <= T(0x1p1000)) {
+                T px = mx, py = my;
+                if (mul2 > T(kEpsSqrt) && r2 > T(0x1.0000000000001p-52)) {
+                    const T y = rsq_nr(r2);  // 1 / rd
+                    T srw, crw;
+                    sincos_0_2((r2 * y) * wf, &srw, &crw);
+                    const T ru = srw * y * c.uk[1];  // sin(rd w) / (rd 2 tan(w / 2))
+                    const T ic = nr_range(fabs(crw)) ? (crw < T(0) ? -rcp_nr(-crw) : rcp_nr(crw))
+                                                     : T(1) / crw;
+                    px = (mx * ru) * ic;
+                    py = (my * ru) * ic;
+                }
+                const T n2 = fma(px, px, fma(py, py, T(1)));
+                const T in = nr_range(n2) ? rsq_nr(n2) : T(1) / sqrt(n2);
+                X = px * in;
+                Y = py * in;
+                Z = in;
+                return ST_OK;
+            }
+        }
+#endif
         T rd = sqrt(mx * mx + my * my);
         T px = mx, py = my;
         if (mul2 > T(kEpsSqrt) && rd > T(kEpsSqrt)) {

@@ -401,8 +401,8 @@ ACM_API int acm_stream_synchronize(void *stream);
  * word the kernel publishes; -1 = auto = 2.
  * ACM_TUNE_SAMPLE_FUSED: acm_sample_points in one pass (unproject once,
  * decoupled look-back for the output offsets; -1 = auto = tiles of 4 x 256
- * cells for every model but Pinhole, whose unprojection is cheap enough
- * that the two-pass path is faster; 1 / 2 / 3 = tiles of 2 / 4 / 8 x 256
+ * cells for every model but Pinhole and FOV, whose unprojections are cheap
+ * enough that the two-pass path is faster; 1 / 2 / 3 = tiles of 2 / 4 / 8 x 256
  * cells) or the two-pass count / scan / recompute-and-write path (0).
  * Outputs are identical for every value.
  * ACM_TUNE_UNPROJECT_RCP: unprojections (acm_unproject, acm_sample_points*)
@@ -418,8 +418,9 @@ ACM_API int acm_stream_synchronize(void *stream);
  * newton_fast): FMA / reciprocal iterates whose every break / continue
  * decision is certified against the reference's, with the reference's own
  * loop for any pixel that cannot be certified (-1 = auto = on, 0 = the
- * reference's loop for every pixel, 1 = on).  Statuses are identical for
- * every value; rays agree within a few ulp.
+ * reference's loop for every pixel, 1 = on); the same knob switches FOV's
+ * unprojection between its reciprocal / polynomial form and the IEEE one.
+ * Statuses are identical for every value; rays agree within a few ulp.
  * ACM_TUNE_UNPROJECT_PPT: acm_unproject's pixels per lane and AoS ray
  * stores (-1 = auto = 2 pixels per lane; for Pinhole, DS, UCM and EUCM each
  * wave's 64 AoS rays staged in LDS and written as 16-B pieces when rays is
