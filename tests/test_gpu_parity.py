@@ -668,3 +668,67 @@ def test_unproject_every_store_form_identical(n):
             L.acm_set_tuning(_lib.TUNE_UNPROJECT_PPT, -1)
         for r, s in outs[1:]:
             assert np.array_equal(r, outs[0][0]) and np.array_equal(s, outs[0][1]), model
+
+
+def test_newton_fast_random_cameras():
+    """Randomised sweep of the certified fast Newton loops: 150 KB and 150
+    RadTan cameras with random intrinsics and distortion (about a third of
+    them beyond the fast loops' per-camera bounds, which must then take the
+    reference loop), 40K pixels each spread over the image and a margin.
+    Statuses with ACM_TUNE_NEWTON_FAST on and off are identical for every
+    pixel, rays within 64 ulp of 1."""
+    import ctypes
+    import torch
+    from apex_camera_models import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(2024)
+    n = 40_000
+    st_on = torch.empty((n,), dtype=torch.uint8, device="cuda")
+    st_off = torch.empty_like(st_on)
+    r_on = torch.empty((n, 3), dtype=torch.float64, device="cuda")
+    r_off = torch.empty_like(r_on)
+    failures = 0
+    covered = {1: [0, 0], 2: [0, 0]}  # [beyond the fast loop's bound, within]
+    try:
+        for model in (2, 1):
+            for _ in range(150):
+                w, h = int(rng.integers(320, 1400)), int(rng.integers(240, 1100))
+                f = rng.uniform(0.3, 1.2) * w
+                base = [f, f * rng.uniform(0.95, 1.05), w * rng.uniform(0.4, 0.6),
+                        h * rng.uniform(0.4, 0.6)]
+                if model == 2:
+                    dist = list(rng.normal(0, [0.2, 0.1, 0.1, 0.15]))
+                    bound = 4 * abs(dist[0]) + 16 * abs(dist[1]) + 64 * abs(dist[2]) + \
+                        256 * abs(dist[3])
+                    covered[model][int(bound <= 63)] += 1
+                else:  # k1 k2 p1 p2 k3
+                    dist = list(rng.normal(0, [0.3, 0.1, 0.005, 0.005, 0.02]))
+                    bound = 8 * abs(dist[0]) + 64 * abs(dist[1]) + 512 * abs(dist[4]) + \
+                        16 * (abs(dist[2]) + abs(dist[3]))
+                    covered[model][int(bound <= 15)] += 1
+                params = base + dist
+                cam = _lib.AcmCamera()
+                _lib.check(L.acm_camera_init(ctypes.byref(cam), model,
+                                             (ctypes.c_double * len(params))(*params),
+                                             len(params), w, h))
+                px = torch.as_tensor(np.stack([rng.uniform(-20, w + 20, n),
+                                               rng.uniform(-20, h + 20, n)], 1), device="cuda")
+                for knob, st, r in ((1, st_on, r_on), (0, st_off, r_off)):
+                    L.acm_set_tuning(_lib.TUNE_NEWTON_FAST, knob)
+                    _lib.check(L.acm_unproject(ctypes.byref(cam), n, px.data_ptr(), r.data_ptr(),
+                                               0, st.data_ptr(), None))
+                torch.cuda.synchronize()
+                if not torch.equal(st_on, st_off):
+                    failures += 1
+                    continue
+                ok = st_off == 0
+                d = (r_on[ok] - r_off[ok]).abs()
+                fin = torch.isfinite(r_off[ok]).all(1)
+                assert torch.equal(fin, torch.isfinite(r_on[ok]).all(1)), (model, params)
+                if fin.any():
+                    assert float(d[fin].max()) <= 64 * 2.0 ** -52, (model, params)
+    finally:
+        L.acm_set_tuning(_lib.TUNE_NEWTON_FAST, -1)
+    assert failures == 0, failures
+    for model in (1, 2):  # both paths of the per-camera switch were exercised
+        assert min(covered[model]) >= 15, covered
