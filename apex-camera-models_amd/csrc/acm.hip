@@ -1242,6 +1242,30 @@ __device__ __forceinline__ bool sample_cell(const Cam<double>& c, const Grid& g,
     return st == ST_OK && Z > 0.0;  // :91-94
 }
 
+// The count pass only needs keep = (status Ok && Z > 0).  For Pinhole that
+// is decidable without the ray: its only status is the image bounds
+// (pinhole.rs:229-235) and Z = 1 / sqrt(1 + r2) (:240-245) is > 0 exactly
+// when 1 + r2 is finite (sqrt >= 1 then; inf gives Z = 0, NaN fails), with
+// mx, my the same correctly rounded quotients -- so the pass skips the
+// square root, the division and the ray.
+template <class TagT>
+__device__ __forceinline__ bool sample_keep(const Cam<double>& c, const Grid& g,
+                                            const CellWalk& w) {
+    double u, v, X, Y, Z;
+    return sample_cell<TagT>(c, g, w, u, v, X, Y, Z);
+}
+template <>
+__device__ __forceinline__ bool sample_keep<Tag<Pinhole>>(const Cam<double>& c, const Grid& g,
+                                                          const CellWalk& w) {
+    const double u = ((double)w.j + 0.5) * g.cw;  // :69
+    const double v = ((double)w.i + 0.5) * g.ch;  // :70
+    const bool out = u < 0.0 || u >= c.w || v < 0.0 || v >= c.h;
+    const double mx = div_by_f(u - c.p[2], c.p[0], c.ifx);
+    const double my = div_by_f(v - c.p[3], c.p[1], c.ify);
+    const double r2 = mx * mx + my * my;
+    return !out && 1.0 + r2 < INFINITY;
+}
+
 // Each workgroup owns kSampleCells consecutive cells (kSampleR rounds of 256):
 // few enough workgroups that the scan of their counts is a handful of
 // coalesced tiles, and round r of lane t is cell base + 256 r + t, so the
@@ -1259,10 +1283,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_count(CamArg cam, Grid g, siz
     cw.init(g, base, threadIdx.x);
     for (int r = 0; r < kSampleR; ++r, cw.step(g)) {
         const size_t cell = base + (size_t)r * kBlock + threadIdx.x;
-        if (cell < cells) {
-            double u, v, X, Y, Z;
-            mine += sample_cell<TagT>(c, g, cw, u, v, X, Y, Z) ? 1u : 0u;
-        }
+        if (cell < cells) mine += sample_keep<TagT>(c, g, cw) ? 1u : 0u;
     }
     __shared__ uint32_t sm[kBlock / 64];
 #pragma unroll
