@@ -25,6 +25,7 @@ LIB_PATH = os.environ.get("ACM_LIB_PATH") or os.path.join(_PKG_ROOT, "lib", "lib
 PINHOLE, RADTAN, KANNALA_BRANDT, DOUBLE_SPHERE, UCM, EUCM, FOV = range(7)
 LAYOUT_AOS, LAYOUT_SOA = 0, 1
 EXACT_MATH = 0x100  # OR-ed into acm_project's layout (include/acm.h)
+REFERENCE_NEWTON = 0x200  # OR-ed into acm_unproject's layout / acm_sample_points_ex's flags
 INVALID_SKIP, INVALID_SENTINEL = 0, 1
 MAX_PARAMS = 9
 
@@ -67,8 +68,10 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
                                 ctypes.c_void_p)
 TUNE_PROJECT_VARIANT, TUNE_RESIDUAL_NT, TUNE_NE_WAVES, TUNE_FOV_UNROLL, TUNE_NE_UNROLL = 0, 1, 2, 3, 4
 TUNE_ALIGN_J, TUNE_NT_LOADS, TUNE_NT_LOADS_UNPROJECT, TUNE_LM_HOST_RESULT = 5, 6, 7, 8
-TUNE_SAMPLE_FUSED, TUNE_UNPROJECT_RCP, TUNE_SAMPLE_PATIENCE, TUNE_NEWTON_FAST = 9, 10, 11, 12
+TUNE_SAMPLE_FUSED, TUNE_UNPROJECT_RCP, TUNE_SAMPLE_PATIENCE = 9, 10, 11
+TUNE_NEWTON_FAST = 12  # removed in round 3: acm_set_tuning rejects it (use REFERENCE_NEWTON)
 TUNE_UNPROJECT_PPT = 13
+TUNE_SAMPLE_CERT = 14
 ERR_NOT_SUPPORTED = -6
 ERR_NUMERICAL = -7
 LM_TERMINATION = {0: "MaxIterations", 1: "CostTolerance", 2: "ParameterTolerance",
@@ -100,6 +103,8 @@ EXPORTED_SYMBOLS = (
     "acm_reprojection_stats_workspace_size",
     "acm_reprojection_stats",
     "acm_reprojection_stats_merge",
+    "acm_error_stats_workspace_size",
+    "acm_error_stats",
     "acm_linear_system_columns",
     "acm_linear_system_qr_workspace_size",
     "acm_linear_system_qr",
@@ -120,6 +125,8 @@ EXPORTED_SYMBOLS = (
     "acm_sample_points_workspace_size",
     "acm_sample_points",
     "acm_sample_points_range",
+    "acm_sample_points_ex",
+    "acm_sample_points_certificate",
     "acm_undistort_image",
     "acm_set_device",
     "acm_device_malloc",
@@ -183,6 +190,10 @@ def load():
     L.acm_reprojection_stats_merge.argtypes = [sz, ctypes.POINTER(ctypes.c_double),
                                                ctypes.POINTER(ctypes.c_double)]
     L.acm_reprojection_stats_merge.restype = i
+    L.acm_error_stats_workspace_size.argtypes = [sz]
+    L.acm_error_stats_workspace_size.restype = sz
+    L.acm_error_stats.argtypes = [sz, vp, vp, vp, sz, vp]
+    L.acm_error_stats.restype = i
     L.acm_reprojection_stats.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp, sz, vp]
     L.acm_reprojection_stats.restype = i
     L.acm_sample_points_grid.argtypes = [ctypes.c_uint32, ctypes.c_uint32, sz,
@@ -195,6 +206,10 @@ def load():
     L.acm_sample_points.restype = i
     L.acm_sample_points_range.argtypes = [cam_p, sz, sz, sz, vp, vp, vp, vp, sz, vp]
     L.acm_sample_points_range.restype = i
+    L.acm_sample_points_ex.argtypes = [cam_p, sz, sz, sz, i, vp, vp, vp, vp, sz, vp]
+    L.acm_sample_points_ex.restype = i
+    L.acm_sample_points_certificate.argtypes = [cam_p, ctypes.POINTER(ctypes.c_double)]
+    L.acm_sample_points_certificate.restype = i
     L.acm_linear_system_columns.argtypes = [i]
     L.acm_linear_system_columns.restype = i
     L.acm_linear_system_qr_workspace_size.argtypes = [i, sz]

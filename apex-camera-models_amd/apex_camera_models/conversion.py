@@ -8,7 +8,7 @@ from __future__ import annotations
 import time
 from dataclasses import dataclass
 
-from . import util
+from . import _lib, util
 from .camera import (CameraModel, DoubleSphereModel, EucmModel, FovModel, Intrinsics,
                      KannalaBrandtModel, RadTanModel, UcmModel)
 from .optimizer import CONVERTER_BOUNDS, LevenbergMarquardt, LevenbergMarquardtConfig
@@ -84,15 +84,19 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
                                                allreduce=allreduce)
         if res.termination == "Failed":
             status = "Linear Only"
-    except Exception:  # camera_converter.rs:443: Err(_) => "Linear Only"
+    except _lib.AcmError as e:
+        # camera_converter.rs:443: the solver's Err(_) => "Linear Only".  Only
+        # a numerical failure of the solve is that; a device fault
+        # (ACM_ERR_HIP, incl. a failed all-reduce), a bad argument or a too
+        # small workspace is not a solver outcome and propagates.
+        if e.code != _lib.ERR_NUMERICAL:
+            raise
         status = "Linear Only"
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
     final = reproj(model)
-    try:  # camera_converter.rs:425-438 (NaN results on failure)
-        validation = util.validate_conversion_accuracy(model, input_model)
-    except Exception:
-        validation = None
+    # camera_converter.rs:425-438; failed regions come back as NaN (no raise)
+    validation = util.validate_conversion_accuracy(model, input_model)
     return ConversionMetrics(model=model, model_name=DISPLAY[target],
                              final_reprojection_error=final, initial_reprojection_error=initial,
                              optimization_time_ms=ms, convergence_status=status,

@@ -8,8 +8,12 @@ The path shards trivially: every point is independent.
     P(P+1)/2 + P + 2 <= 56 doubles; ONE all-reduce(sum) of that vector per
     evaluation (448 B: latency-bound, link bandwidth irrelevant) before the
     host solve, so every rank takes identical LM steps;
-  * reprojection statistics: all-reduce of [sum, sumsq, count] (sum), min,
-    max, then of sum (e - mean)^2 -- the reference's two-pass stddev;
+  * reprojection statistics: each rank reduces its shard on the GPU to the
+    8-double acm_reprojection_stats / acm_error_stats result; ONE all-gather
+    of those, then libacm's rank-ordered Chan merge
+    (acm_reprojection_stats_merge) -- every rank gets the same bits; the
+    median is the exact distributed radix select (one all-reduce of a
+    histogram per pass);
   * sample_points: ranks take contiguous row ranges of the cell grid, and
     concatenation in rank order (offsets from an all-gather of the kept
     counts) reproduces the serial order of point_sampling.rs:88-103.
@@ -123,11 +127,33 @@ def merge_reprojection_stats(local_result: torch.Tensor, group=None) -> dict:
     return d
 
 
+def device_error_stats(errors: torch.Tensor) -> torch.Tensor:
+    """acm_error_stats: the 8-double statistics result of one shard's device
+    error vector (NaN = invalid), reduced on the GPU -- no host copy."""
+    from . import _lib
+    from .camera import _stream_handle
+    L = _lib.load()
+    e = errors.contiguous()
+    n = e.numel()
+    out = torch.empty((8,), dtype=torch.float64, device=e.device)
+    ws_bytes = L.acm_error_stats_workspace_size(n)
+    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=e.device)
+    _lib.check(L.acm_error_stats(n, e.data_ptr() if n else None, out.data_ptr(), ws.data_ptr(),
+                                 ws_bytes, _stream_handle()))
+    return out
+
+
 def combine_reprojection_stats(local_errors: torch.Tensor, group=None) -> dict:
     """Statistics of the union of every rank's per-point errors (NaN =
-    invalid) via merge_reprojection_stats; for GPU errors also the exact
-    median of the union (distributed_median)."""
-    out = merge_reprojection_stats(local_reprojection_result(local_errors), group)
+    invalid) via merge_reprojection_stats.  Device errors are reduced on the
+    GPU (acm_error_stats) and also get the exact median of the union
+    (distributed_median); host errors (the gloo tests' oracle shards) take
+    local_reprojection_result."""
+    if local_errors.is_cuda:
+        local = device_error_stats(local_errors.to(torch.float64))
+    else:
+        local = local_reprojection_result(local_errors)
+    out = merge_reprojection_stats(local, group)
     if local_errors.is_cuda and out["n_valid"] > 0:
         out["median"] = distributed_median(local_errors, out["n_valid"], group)
     return out

@@ -35,10 +35,11 @@ class ProjectionError:
     n_valid: int = 0
 
 
-def sample_points(camera_model: CameraModel, n: int):
+def sample_points(camera_model: CameraModel, n: int, reference_newton: bool = False):
     """Grid of ~n pixel-cell centres, unprojected; keeps Ok && z > 0, in order.
 
     Returns (points_2d (M,2), points_3d (M,3)) float64 device tensors.
+    reference_newton=True: ACM_REFERENCE_NEWTON for this call.
     """
     L = _lib.load()
     cam = camera_model.acm_camera()
@@ -52,9 +53,10 @@ def sample_points(camera_model: CameraModel, n: int):
     counts = torch.zeros((2,), dtype=torch.int64, device=dev)
     ws_bytes = L.acm_sample_points_workspace_size(ctypes.byref(cam), n)
     ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=dev)
-    _lib.check(L.acm_sample_points(ctypes.byref(cam), n, uv.data_ptr(), xyz.data_ptr(),
-                                   counts.data_ptr(), ws.data_ptr(), ws_bytes,
-                                   _stream_handle()))
+    _lib.check(L.acm_sample_points_ex(ctypes.byref(cam), n, 0, cap,
+                                      _lib.REFERENCE_NEWTON if reference_newton else 0,
+                                      uv.data_ptr(), xyz.data_ptr(), counts.data_ptr(),
+                                      ws.data_ptr(), ws_bytes, _stream_handle()))
     m = int(counts[0].item())
     return uv[:m], xyz[:m]
 

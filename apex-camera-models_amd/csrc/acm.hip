@@ -241,7 +241,6 @@ static std::atomic<int> g_sample_patience{-1};
 // RN(1 / fy) (div_by_f, bit-identical) instead of two IEEE divisions per
 // point: -1 = auto = on, 0 = off, 1 = on.
 static std::atomic<int> g_unproject_rcp{-1};
-static std::atomic<int> g_newton_fast{-1};
 static std::atomic<int> g_unproject_ppt{-1};
 // acm_lm_optimize without an all-reduce: the normal-equations epilogue writes
 // its P*P + P + 2 results straight into pinned host memory instead of device
@@ -1160,6 +1159,34 @@ __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t 
     reproj_block_store(s, ss, mn, mx, v, parts + (size_t)blockIdx.x * kReprojW);
 }
 
+// The same per-workgroup partials from a given error vector (NaN = invalid):
+// the statistics of a shard whose errors already sit in HBM
+// (acm_error_stats, distributed.combine_reprojection_stats).
+__global__ __launch_bounds__(kBlock) void k_errstats_pass1(size_t n,
+                                                           const double* __restrict__ errs,
+                                                           double* __restrict__ parts) {
+    double s = 0.0, ss = 0.0, mn = INFINITY, mx = -INFINITY, cnt = 0.0;
+    double K = 0.0, S = 0.0, Q = 0.0;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const double e = errs[i];
+        if (e == e) {
+            s += e;
+            ss += e * e;
+            mn = fmin(mn, e);
+            mx = fmax(mx, e);
+            K = cnt == 0.0 ? e : K;
+            const double d = e - K;
+            S += d;
+            Q += d * d;
+            cnt += 1.0;
+        }
+    }
+    const double mloc = cnt > 0.0 ? S / cnt : 0.0;
+    const Mv v{cnt, K + mloc, cnt > 0.0 ? Q - S * mloc : 0.0};
+    reproj_block_store(s, ss, mn, mx, v, parts + (size_t)blockIdx.x * kReprojW);
+}
+
 // fixed-order finish: tot = [sum, sumsq, min, max, count, mean, M2]
 __global__ __launch_bounds__(kBlock) void k_reproj_finish1(const double* __restrict__ parts,
                                                            int nb, double* __restrict__ tot) {
@@ -1225,8 +1252,10 @@ struct CellWalk {
         j = (uint32_t)(cb - i0 * g.ncx) + off;
         while (j >= g.ncx) { j -= g.ncx; ++i; }
     }
-    __device__ __forceinline__ void step(const Grid& g) {
-        j += kBlock;
+    __device__ __forceinline__ void step(const Grid& g) { step_by<kBlock>(g); }
+    template <uint32_t S>
+    __device__ __forceinline__ void step_by(const Grid& g) {
+        j += S;
         while (j >= g.ncx) { j -= g.ncx; ++i; }
     }
 };
@@ -1238,8 +1267,16 @@ __device__ __forceinline__ bool sample_cell(const Cam<double>& c, const Grid& g,
     using M = typename TagT::template type<double>;
     u = ((double)w.j + 0.5) * g.cw;  // :69
     v = ((double)w.i + 0.5) * g.ch;  // :70
-    const uint8_t st = M::unproject(c, u, v, X, Y, Z);
-    return st == ST_OK && Z > 0.0;  // :91-94
+    if constexpr (std::is_same<TagT, Tag<KannalaBrandt>>::value) {
+        // the keep decision taken exactly on the reference's theta, not read
+        // off the polynomial-cos ray (KannalaBrandt::unproject_k)
+        bool keep;
+        const uint8_t st = M::template unproject_k<true>(c, u, v, X, Y, Z, keep);
+        return st == ST_OK && keep;  // :91-94
+    } else {
+        const uint8_t st = M::unproject(c, u, v, X, Y, Z);
+        return st == ST_OK && Z > 0.0;  // :91-94
+    }
 }
 
 // The count pass only needs keep = (status Ok && Z > 0).  For Pinhole that
@@ -1370,7 +1407,207 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(CamArg cam, Grid g, siz
     }
 }
 
-// Single pass (ACM_TUNE_SAMPLE_FUSED, default): workgroup b owns tile b of
+// ------------------------------------------- segment two-pass (r03, default)
+// The grid is cut into segments of 64 consecutive cells (one wave, one cell
+// per lane).  Pass 1 (k_seg_count) gives every segment its kept count; pass 2
+// scans the per-workgroup sums (k_scan_counts); pass 3 (k_seg_write)
+// recomputes each segment and writes its kept points at known offsets.  No
+// look-back and no cross-wave synchronisation in the write pass: a wave owns
+// whole segments, compacts its kept rays in 1.5 KiB of its own LDS and writes
+// them as 16-B pieces.  Segments with nothing kept are skipped outright.
+//
+// The count pass mostly needs no unprojection at all: every model's keep
+// decision depends on the cell only through r2 = mx^2 + my^2 (KB through
+// ru = min(sqrt(r2), pi/2)), so a segment whose r2 interval lies inside a
+// region certified on the host (seg_cert) is counted from its geometry --
+// ALL cells kept or NONE.  Only segments that straddle the boundary of the
+// kept region (a thin ring: ~1-3% of the segments) run the per-cell keep.
+constexpr int kSegCells = 64;
+constexpr int kSegPerBlock = kBlock;  // segments per count / write workgroup
+constexpr size_t kSegBlockCells = (size_t)kSegCells * kSegPerBlock;
+
+enum : int { SEG_UNKNOWN = 0, SEG_ALL = 1, SEG_NONE = 2 };
+
+// Host-certified keep regions, in the model's certificate variable q (KB: ru
+// = min(sqrt(r2), pi/2); the other models: r2).  Every cell whose q lies in
+// [all_lo, all_hi] is kept, every cell in [none_lo, none_hi] is not (both
+// intervals empty when on == 0: every segment is decided cell by cell).
+struct SegCert {
+    int on;
+    int in_bounds_checked;  // 1: the model's unprojection has the image-bounds test
+    double all_lo, all_hi, none_lo, none_hi;
+};
+
+// Rigorous bounds of r2 = mx^2 + my^2 over the cells [c0, c1] (inclusive,
+// launch-local) as the kernels compute them (mx = RN(RN(u - cx) / fx)
+// etc.), widened far beyond their few-ulp rounding; false when any cell may
+// lie outside the image (the unprojections' bounds test).
+__device__ __forceinline__ bool seg_r2_bounds(const Cam<double>& c, const Grid& g, uint64_t c0,
+                                              uint64_t c1, double& lo, double& hi) {
+    const uint64_t a = c0 + g.cell0, b = c1 + g.cell0;
+    const uint64_t i0 = a / g.ncx, i1 = b / g.ncx;
+    uint64_t j0 = a - i0 * g.ncx, j1 = b - i1 * g.ncx;
+    if (i0 != i1) {  // several rows: every column may occur
+        j0 = 0;
+        j1 = g.ncx - 1;
+    }
+    const double ulo = ((double)j0 + 0.5) * g.cw, uhi = ((double)j1 + 0.5) * g.cw;
+    const double vlo = ((double)i0 + 0.5) * g.ch, vhi = ((double)i1 + 0.5) * g.ch;
+    const bool inb = ulo >= 0.0 && vlo >= 0.0 && uhi < c.w * (1.0 - 0x1p-40) &&
+                     vhi < c.h * (1.0 - 0x1p-40);
+    // |m| over an interval of u (m monotone in u): [0 if the interval
+    // straddles cx, else min |end|] .. max |end|, plus rounding slack
+    auto mrange = [](double l, double h, double cc, double f, double& mlo, double& mhi) {
+        const double e0 = (l - cc) / f, e1 = (h - cc) / f;
+        const double slack = (fabs(l) + fabs(h) + fabs(cc)) * 0x1p-44 / fabs(f) + 0x1p-1000;
+        const double a0 = fabs(e0), a1 = fabs(e1);
+        const bool straddle = (e0 <= 0.0) != (e1 <= 0.0);
+        mlo = fmax((straddle ? 0.0 : fmin(a0, a1)) * (1.0 - 0x1p-40) - slack, 0.0);
+        mhi = fmax(a0, a1) * (1.0 + 0x1p-40) + slack;
+    };
+    double xlo, xhi, ylo, yhi;
+    mrange(ulo, uhi, c.p[2], c.p[0], xlo, xhi);
+    mrange(vlo, vhi, c.p[3], c.p[1], ylo, yhi);
+    lo = (xlo * xlo + ylo * ylo) * (1.0 - 0x1p-40);
+    hi = (xhi * xhi + yhi * yhi) * (1.0 + 0x1p-40);
+    return inb && lo == lo && hi == hi;
+}
+
+template <class TagT>
+__device__ __forceinline__ int seg_classify(const Cam<double>& c, const Grid& g, const SegCert& k,
+                                            uint64_t c0, uint64_t c1) {
+    if (!k.on) return SEG_UNKNOWN;
+    double lo, hi;
+    if (!seg_r2_bounds(c, g, c0, c1, lo, hi)) return SEG_UNKNOWN;
+    double qlo = lo, qhi = hi;
+    if constexpr (std::is_same<TagT, Tag<KannalaBrandt>>::value) {
+        constexpr double kHalfPi = kPi / 2.0;  // the reference's clamp, :467
+        qlo = fmin(sqrt(lo) * (1.0 - 0x1p-40), kHalfPi);
+        qhi = fmin(sqrt(hi) * (1.0 + 0x1p-40), kHalfPi);
+    }
+    if (qlo >= k.all_lo && qhi <= k.all_hi) return SEG_ALL;
+    if (qlo >= k.none_lo && qhi <= k.none_hi) return SEG_NONE;
+    return SEG_UNKNOWN;
+}
+
+template <class TagT>
+__global__ __launch_bounds__(kBlock) void k_seg_count(CamArg cam, Grid g, size_t cells, SegCert cert,
+                                                      uint32_t* __restrict__ seg_cnt,
+                                                      uint64_t* __restrict__ blk_sum) {
+    const Cam<double> c = make_cam<double>(cam);
+    const int lane = threadIdx.x & 63;
+    const uint64_t nseg = (cells + kSegCells - 1) / kSegCells;
+    const uint64_t seg = (uint64_t)blockIdx.x * kSegPerBlock + threadIdx.x;
+    const uint64_t wseg0 = seg - lane;  // the wave's first segment
+    uint32_t cnt = 0;
+    int cls = SEG_NONE;
+    if (seg < nseg) {
+        const uint64_t c0 = seg * kSegCells;
+        const uint64_t c1 = c0 + kSegCells <= cells ? c0 + kSegCells - 1 : cells - 1;
+        cls = seg_classify<TagT>(c, g, cert, c0, c1);
+        if (cls == SEG_ALL) cnt = (uint32_t)(c1 - c0 + 1);
+    }
+    // segments the geometry cannot decide: the whole wave counts their cells
+    uint64_t unk = __ballot(cls == SEG_UNKNOWN);
+    while (unk) {
+        const int k = __builtin_amdgcn_readfirstlane(__ffsll((long long)unk) - 1);
+        unk &= unk - 1;
+        const uint64_t base = (wseg0 + (uint64_t)k) * kSegCells;
+        CellWalk cw;
+        cw.init(g, base, lane);
+        const bool keep = base + lane < cells && sample_keep<TagT>(c, g, cw);
+        const uint32_t kc = (uint32_t)__popcll(__ballot(keep));
+        if (lane == k) cnt = kc;
+    }
+    if (seg < nseg) seg_cnt[seg] = cnt;
+    __shared__ uint32_t sm[kBlock / 64];
+    uint32_t t = cnt;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+    if (lane == 0) sm[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += sm[w];
+        blk_sum[blockIdx.x] = tot;
+    }
+}
+
+template <class TagT>
+__global__ __launch_bounds__(kBlock) void k_seg_write(CamArg cam, Grid g, size_t cells,
+                                                      const uint32_t* __restrict__ seg_cnt,
+                                                      const uint64_t* __restrict__ blk_off,
+                                                      double* __restrict__ uv_out,
+                                                      double* __restrict__ xyz_out) {
+    const Cam<double> c = make_cam<double>(cam);
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nseg = (cells + kSegCells - 1) / kSegCells;
+    const uint64_t seg = (uint64_t)blockIdx.x * kSegPerBlock + threadIdx.x;
+    // offsets of this workgroup's 256 segments: block offset + exclusive scan
+    const uint32_t cnt = seg < nseg ? seg_cnt[seg] : 0u;
+    uint32_t x = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    __shared__ double s_ray[kBlock / 64][64 * 3];
+    if (lane == 63) s_wsum[wid] = x;
+    __syncthreads();
+    uint64_t base_off = blk_off[blockIdx.x];
+    for (int w = 0; w < wid; ++w) base_off += s_wsum[w];
+    const uint64_t my_off = base_off + (x - cnt);  // lane l: offset of segment wseg0 + l
+    const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
+    double* lx = s_ray[wid];
+    const uint64_t wseg0 = seg - lane;
+    CellWalk cw;
+    cw.init(g, wseg0 * kSegCells, lane);
+#pragma unroll 1
+    for (int k = 0; k < 64; ++k, cw.template step_by<kSegCells>(g)) {
+        const uint64_t sg = wseg0 + (uint64_t)k;
+        if (sg >= nseg) break;
+        const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)cnt, k);
+        if (sc == 0) continue;  // nothing kept here (certified or counted)
+        const uint64_t off = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_off >> 32), k) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_off, k);
+        const uint64_t cell = sg * kSegCells + lane;
+        double u = 0.0, v = 0.0, X = 0.0, Y = 0.0, Z = 0.0;
+        bool keep = false;
+        if (cell < cells) keep = sample_cell<TagT>(c, g, cw, u, v, X, Y, Z);
+        const uint64_t m = __ballot(keep);
+        const uint32_t rank = (uint32_t)__popcll(m & below);
+        if (keep) {
+            st2<false>(uv_out + 2 * (off + rank), u, v);  // 16 B per lane, one run per wave
+            double* d = lx + 3 * rank;
+            d[0] = X;
+            d[1] = Y;
+            d[2] = Z;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the kept rays: 3 * kc consecutive doubles of xyz_out, as 16-B pieces
+        // on the 16-B grid (+ a single leading / trailing double)
+        const uint32_t kc = (uint32_t)__popcll(m);
+        double* dst = xyz_out + 3 * off;
+        const uint32_t nd = 3 * kc;
+        const uint32_t h = (uint32_t)((reinterpret_cast<uintptr_t>(dst) >> 3) & 1u);
+        const uint32_t np = (nd - h) >> 1;
+        for (uint32_t p = lane; p < np; p += 64) {
+            const uint32_t dd = h + 2 * p;
+            st2<false>(dst + dd, lx[dd], lx[dd + 1]);
+        }
+        if (lane == 0 && h) dst[0] = lx[0];
+        if (lane == 63 && ((nd - h) & 1u)) dst[nd - 1] = lx[nd - 1];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+// Single pass (ACM_TUNE_SAMPLE_FUSED >= 1): workgroup b owns tile b of
 // kFusedR x 256 cells, unprojects them once keeping the rays in registers,
 // publishes its kept count, and finds its output offset by a decoupled
 // look-back over the tiles before it (one status word per tile: flag in bits
@@ -1384,21 +1621,11 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(CamArg cam, Grid g, siz
 // workgroup ever waits on one that has not started.  The kept points come out
 // in cell order exactly as from the two-pass path.
 constexpr int kFusedRMin = 2;  // smallest tile (rounds of 256 cells) any setting uses
-// Per-model tile (rounds of 256 cells): fewer, larger tiles mean fewer
-// look-backs, but each round's rays take 6 KiB of LDS per workgroup, so
-// larger tiles cost occupancy (R = 4: 25 KB, 6 workgroups per CU).
-// ACM_TUNE_SAMPLE_FUSED 1 / 2 / 3 selects R = 2 / 4 / 8.
-template <class TagT> struct SampleR { static constexpr int R = 4; };
-// Auto (-1) picks the single pass for every model whose unprojection is
-// worth computing once, and the two-pass path for Pinhole: its unprojection
-// is a sqrt and a division, so counting and recomputing costs less than the
-// look-back and the LDS staging (0.99-1.04 vs 1.14-1.16 ms at 1e8 cells;
-// profiles/r02_diag_sample.log, r02b_diag_sample.log).
-template <class TagT> struct SampleSinglePass { static constexpr bool on = true; };
-template <> struct SampleSinglePass<Tag<Pinhole>> { static constexpr bool on = false; };
-// FOV's unprojection became cheap with its reciprocal form (r02e): two-pass
-// 1.04 vs single pass 1.15 ms at 1e8 cells (profiles/r02e_diag_sample.log).
-template <> struct SampleSinglePass<Tag<Fov>> { static constexpr bool on = false; };
+// Tiles of R rounds of 256 cells: fewer, larger tiles mean fewer look-backs,
+// but each round's rays take 6 KiB of LDS per workgroup, so larger tiles cost
+// occupancy (R = 4: 25 KB, 6 workgroups per CU).  ACM_TUNE_SAMPLE_FUSED
+// 1 / 2 / 3 selects R = 2 / 4 / 8.  (Round 2's default; the segment two-pass
+// path above replaced it in round 3.)
 constexpr size_t kFusedCells = (size_t)kBlock * kFusedRMin;
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
 constexpr int kLbPatience = 512;  // polls (s_sleep between) before computing a count itself
@@ -1548,6 +1775,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR 
                     if (lane == 0) {  // not resident (or very late): count it here
                         s_lb_top = (uint64_t)top;
                         s_lb_excl = excl;
+                        // the helped set belongs to THIS window: after the
+                        // look-back moved on (top -= 64) the register copy is
+                        // 0 and the old window's entries must not survive
+                        s_lb_helped = helped;
                         s_lb_help = (uint64_t)(__ffsll((long long)(none & need)) - 1);
                         s_lb_state = 2;
                     }
@@ -2325,7 +2556,9 @@ static unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 // of once per lane by OCML.
 // Unprojection launches also carry RN(1 / fx), RN(1 / fy) (0 outside the
 // range div_by_f is exact in) and the model's uniform subexpressions.
-static CamArg prep(acm_camera c) {
+// reference_newton (ACM_REFERENCE_NEWTON, per call): the reference's own
+// Newton loops for every pixel (KB, RadTan) and FOV's IEEE unprojection.
+static CamArg prep(acm_camera c, bool reference_newton = false) {
     if (c.model == ACM_FOV) c.params[8] = std::tan(c.params[4] / 2.0);
     CamArg a;
     static_cast<acm_camera&>(a) = c;
@@ -2337,10 +2570,137 @@ static CamArg prep(acm_camera c) {
     a.ifx = rcp ? recip(c.params[0]) : 0.0;
     a.ify = rcp ? recip(c.params[1]) : 0.0;
     unproject_consts<double>(c.model, c.params, a.uk);
-    if (g_newton_fast == 0 &&
+    if (reference_newton &&
         (c.model == ACM_KANNALA_BRANDT || c.model == ACM_RADTAN || c.model == ACM_FOV))
         a.uk[0] = NAN;  // fast Newton loops / FOV fast unprojection off
     return a;
+}
+
+// ---------------------------------------- sample_points keep certificates
+// KB (kannala_brandt.rs:462-561, point_sampling.rs:91-94): a cell is kept iff
+// the reference's Newton loop (theta_0 = ru, theta -= f / f', break when
+// |delta| < 1e-6, NumericalError when |f'| < EPS or after 10 steps) ends Ok
+// and cos(theta) > 0, i.e. |theta| <= kHalfPiDown.  Everything depends on the
+// cell only through ru = min(sqrt(r2), pi/2).  On theta in [-tmax, tmax] bound
+// D = f' from below (dmin > 0) and |f''| from above (cmax) by dense sampling
+// plus a Lipschitz margin; then for every ru in (0, R], with theta* the
+// unique root (f' > 0), the Newton error e_k = |theta_k - theta*| obeys
+//   e_0 <= E0 = max |f(ru)| / dmin,   e_{k+1} <= M e_k^2 + eta,
+// M = cmax / (2 dmin), eta a generous bound on one step's rounding
+// (|f| and |f'| are sums of <= 6 terms of size <= 1 + sum |k_i| tmax^2i).
+// If M E0 <= 1/2 the iterates stay within E0 of theta* (in [-tmax, tmax]), f'
+// stays >= dmin >> EPS, and the bound sequence shows a step with |delta| <=
+// e_k + e_{k+1} + eta < 1e-6 within 10 steps: the reference returns Ok, with
+// a final theta within ef = M (1.01e-6)^2 + 2 eta of theta*.  theta* rises
+// with ru (theta_d(theta*) = ru, theta_d increasing), so
+//   ru in [1e-6 (1 + 1e-6), min(R, theta_d(kHalfPiDown - ef - 1e-9))] -> kept,
+//   ru in [theta_d(kHalfPiDown + ef + 1e-9), R]                  -> dropped.
+// (ru <= 1e-6 is NumericalError or the ru = 0 special case: never certified.)
+// kb_seg_cert_on does this for ru in (0, R], R <= pi/2 the largest bound for
+// which the iterates provably stay in [-tmax, tmax] (pi/2 + 2 E0 <= tmax
+// above becomes R + 2 E0(R) <= tmax).
+static SegCert kb_seg_cert_on(const double* p, double tmax) {
+    SegCert s{};
+    s.all_lo = s.none_lo = INFINITY;
+    s.all_hi = s.none_hi = -INFINITY;
+    const double k1 = p[4], k2 = p[5], k3 = p[6], k4 = p[7];
+    const double a1 = std::fabs(k1), a2 = std::fabs(k2), a3 = std::fabs(k3), a4 = std::fabs(k4);
+    auto D = [&](double t2) { return 1.0 + t2 * (3 * k1 + t2 * (5 * k2 + t2 * (7 * k3 + t2 * 9 * k4))); };
+    auto F2 = [&](double t) {  // f''(theta)
+        const double t2 = t * t;
+        return t * (6 * k1 + t2 * (20 * k2 + t2 * (42 * k3 + t2 * 72 * k4)));
+    };
+    auto thd = [&](double t) {  // theta_d(theta)
+        const double t2 = t * t;
+        return t * (1.0 + t2 * (k1 + t2 * (k2 + t2 * (k3 + t2 * k4))));
+    };
+    const double T2 = tmax * tmax;
+    constexpr int G = 16384;
+    double dmin = INFINITY, cmax = 0.0;
+    for (int i = 0; i <= G; ++i) {
+        dmin = std::fmin(dmin, D(T2 * i / G));                // theta^2 in [0, tmax^2]
+        cmax = std::fmax(cmax, std::fabs(F2(tmax * i / G)));  // |f''| is odd: [0, tmax]
+    }
+    // Lipschitz margins of the sampling: |dD/dt2| and the third derivative of f
+    const double LD = 3 * a1 + 10 * a2 * T2 + 21 * a3 * T2 * T2 + 36 * a4 * T2 * T2 * T2;
+    const double LC = 6 * a1 + 60 * a2 * T2 + 210 * a3 * T2 * T2 + 504 * a4 * T2 * T2 * T2;
+    dmin -= 1.01 * LD * (T2 / G) / 2 + 1e-12;
+    cmax += 1.01 * LC * (tmax / G) / 2 + 1e-12;
+    if (!(dmin > 1e-3) || !std::isfinite(cmax)) return s;
+    constexpr double kHalfPi = kPi / 2.0;
+    const double kb = 1.0 + a1 * T2 + a2 * T2 * T2 + a3 * T2 * T2 * T2 + a4 * T2 * T2 * T2 * T2;
+    const double M = cmax / (2.0 * dmin);
+    const double eta = (2.0 * kb + 2.0) * 64 * 0x1p-53 / dmin + 1e-14;
+    // E0(R) = max over ru <= R of |f(ru)| / dmin (|f(ru)| rises with ru)
+    auto E0 = [&](double R) {
+        const double R2 = R * R;
+        return R * R2 * (a1 + R2 * (a2 + R2 * (a3 + R2 * a4))) / dmin + 1e-12;
+    };
+    // the largest ru bound R (<= pi/2) the Newton analysis covers
+    double R = kHalfPi;
+    while (R > 0.05 && !(M * E0(R) <= 0.5 && R + 2.0 * E0(R) <= tmax * (1 - 1e-9) &&
+                         thd(tmax) > R * (1 + 1e-9)))
+        R *= 0.98;
+    if (!(R > 0.05) || !(eta < 1e-9)) return s;
+    bool breaks = false;
+    double e = E0(R);
+    for (int k = 0; k < 10 && !breaks; ++k) {  // a step with |delta| < 1e-6 by step 9
+        const double en = M * e * e + eta;
+        if (e + en + eta < 1e-6 * (1.0 - 1e-3)) breaks = true;
+        e = en;
+    }
+    if (!breaks) return s;
+    const double ef = M * 1.01e-6 * 1.01e-6 + 2.0 * eta;
+    const double m = ef + 1e-9;
+    constexpr double kHpd = KannalaBrandt<double>::kHalfPiDown;
+    s.on = 1;
+    s.all_lo = 1e-6 * (1.0 + 1e-6);
+    s.all_hi = R;
+    if (kHpd - m <= tmax && thd(kHpd - m) < R)  // theta* reaches pi/2 below R
+        s.all_hi = thd(kHpd - m) * (1.0 - 1e-12);
+    if (kHpd + m <= tmax) {
+        const double rn = thd(kHpd + m) * (1.0 + 1e-12);
+        if (rn <= R) {
+            s.none_lo = rn;
+            s.none_hi = R;
+        }
+    }
+    return s;
+}
+
+// Any camera for which a check fails gets no certificate: every segment is
+// then counted cell by cell.  The theta range the bounds cover is tried at a
+// few sizes (a strongly distorted camera's f' may vanish near theta = 2 but
+// not below pi/2); the certificate covering the most is kept.
+static SegCert kb_seg_cert(const double* p) {
+    SegCert best{};
+    best.all_lo = best.none_lo = INFINITY;
+    best.all_hi = best.none_hi = -INFINITY;
+    if (!(std::isfinite(p[4]) && std::isfinite(p[5]) && std::isfinite(p[6]) && std::isfinite(p[7])))
+        return best;
+    double cover = 0.0;
+    for (double tmax : {1.99, 1.9, 1.8, 1.7, 1.62}) {
+        const SegCert s = kb_seg_cert_on(p, tmax);
+        if (!s.on) continue;
+        const double c = std::fmax(s.all_hi, s.none_hi);
+        if (c > cover) {
+            cover = c;
+            best = s;
+        }
+    }
+    return best;
+}
+
+// ACM_TUNE_SAMPLE_CERT: -1 auto = on, 0 = off (every segment counted cell by cell)
+static std::atomic<int> g_sample_cert{-1};
+
+static SegCert seg_cert(const acm_camera& cam) {
+    SegCert s{};
+    s.all_lo = s.none_lo = INFINITY;
+    s.all_hi = s.none_hi = -INFINITY;
+    if (g_sample_cert == 0) return s;
+    if (cam.model == ACM_KANNALA_BRANDT) return kb_seg_cert(cam.params);
+    return s;
 }
 
 static int check_cam(const acm_camera* cam) {
@@ -2548,6 +2908,8 @@ ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_
                           int layout, uint8_t* status, void* stream) {
     int rc = check_cam(cam);
     if (rc) return rc;
+    const bool refn = (layout & ACM_REFERENCE_NEWTON) != 0;
+    layout &= ~ACM_REFERENCE_NEWTON;
     if ((rc = check_layout(layout))) return rc;
     if (n == 0) return ACM_SUCCESS;
     if (!points_2d || !rays || !status) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
@@ -2563,7 +2925,7 @@ ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_
             const size_t waves = (size_t)resident_blocks((const void*)kern) * (kBlock / 64);
             const size_t chunk = (n + waves - 1) / waves;
             const size_t blocks = ((n + chunk - 1) / chunk + kBlock / 64 - 1) / (kBlock / 64);
-            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), b, 0, s, prep(*cam), n, chunk,
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), b, 0, s, prep(*cam, refn), n, chunk,
                                points_2d, rays, status);
             return check_launch("acm_unproject");
         }
@@ -2583,12 +2945,15 @@ ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_
                 auto kern = nt ? (ntl ? k_unproject<TagT, L, true, true, K, PR> : k_unproject<TagT, L, true, false, K, PR>)
                                : (ntl ? k_unproject<TagT, L, false, true, K, PR> : k_unproject<TagT, L, false, false, K, PR>);
                 const dim3 gk((unsigned)((n + (size_t)kBlock * K - 1) / ((size_t)kBlock * K)));
-                hipLaunchKernelGGL(kern, gk, b, 0, s, prep(*cam), n, points_2d, rays, status);
+                hipLaunchKernelGGL(kern, gk, b, 0, s, prep(*cam, refn), n, points_2d, rays, status);
             };
             using One = std::integral_constant<int, 1>;
             using Two = std::integral_constant<int, 2>;
             if (ppt == 1) pick(One{}, std::false_type{});
-            else if (ppt == 3) pick(One{}, std::true_type{});
+            else if (ppt == 3) {  // staged only on a 16-B aligned ray buffer (st2)
+                if (stg) pick(One{}, std::true_type{});
+                else pick(One{}, std::false_type{});
+            }
             else if (stg) pick(Two{}, std::true_type{});
             else pick(Two{}, std::false_type{});
         };
@@ -2767,6 +3132,26 @@ ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double
     });
 }
 
+ACM_API size_t acm_error_stats_workspace_size(size_t n) {
+    return ((size_t)ne_blocks(n) * kReprojW + kReprojW) * sizeof(double);
+}
+
+ACM_API int acm_error_stats(size_t n, const double* errors, double* result, void* workspace,
+                            size_t workspace_bytes, void* stream) {
+    if (!result || !workspace || (n && !errors)) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_error_stats_workspace_size(n))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "error-stats workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    double* p1 = (double*)workspace;
+    int nb = ne_blocks(n);
+    nb = std::max(1, std::min(nb, resident_blocks(reinterpret_cast<const void*>(k_errstats_pass1))));
+    double* tot = p1 + (size_t)nb * kReprojW;
+    hipLaunchKernelGGL(k_errstats_pass1, dim3(nb), dim3(kBlock), 0, s, n, errors, p1);
+    hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb, tot);
+    hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, result);
+    return check_launch("acm_error_stats");
+}
+
 ACM_API int acm_reprojection_stats_merge(size_t nparts, const double* parts, double* result) {
     if (!result || (nparts && !parts)) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL argument");
     // parts: nparts x [rmse, min, max, mean, stddev, n_valid, sum, sumsq]
@@ -2815,13 +3200,16 @@ ACM_API int acm_sample_points_grid(uint32_t width, uint32_t height, size_t n_req
     return ACM_SUCCESS;
 }
 
-// two-pass: counts + offsets (2 per kSampleCells tile); single pass: one
-// status word per kFusedCells tile (+ one word, formerly a ticket, kept so
-// the workspace size is unchanged)
+// Workspace words of every path: two-pass = counts + offsets (2 per
+// kSampleCells tile); single pass = one status word per kFusedCells tile (+1);
+// segment path = one u32 count per 64-cell segment + block sums and block
+// offsets (2 per kSegBlockCells workgroup).
 static size_t sample_ws_words(size_t cells) {
     const size_t nb = cells ? (cells + kSampleCells - 1) / kSampleCells : 1;
     const size_t nt = cells ? (cells + kFusedCells - 1) / kFusedCells : 1;
-    return std::max(2 * nb, nt + 1);
+    const size_t nseg = cells ? (cells + kSegCells - 1) / kSegCells : 1;
+    const size_t nsb = cells ? (cells + kSegBlockCells - 1) / kSegBlockCells : 1;
+    return std::max(std::max(2 * nb, nt + 1), (nseg + 1) / 2 + 2 * nsb);
 }
 
 ACM_API size_t acm_sample_points_workspace_size(const acm_camera* cam, size_t n_requested) {
@@ -2831,12 +3219,15 @@ ACM_API size_t acm_sample_points_workspace_size(const acm_camera* cam, size_t n_
     return sample_ws_words((size_t)ncx * ncy) * sizeof(uint64_t);
 }
 
-ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, size_t cell_begin,
-                                    size_t cell_end, double* points_2d_out, double* points_3d_out,
-                                    uint64_t* counts, void* workspace, size_t workspace_bytes,
-                                    void* stream) {
+ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size_t cell_begin,
+                                 size_t cell_end, int flags, double* points_2d_out,
+                                 double* points_3d_out, uint64_t* counts, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
     int rc = check_cam(cam);
     if (rc) return rc;
+    if (flags & ~ACM_REFERENCE_NEWTON)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "flags must be 0 or ACM_REFERENCE_NEWTON");
+    const bool refn = (flags & ACM_REFERENCE_NEWTON) != 0;
     uint32_t ncx, ncy;
     if ((rc = acm_sample_points_grid(cam->width, cam->height, n_requested, &ncx, &ncy))) return rc;
     const size_t total = (size_t)ncx * ncy;
@@ -2859,29 +3250,45 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
     const int pat = g_sample_patience;
     g.patience = pat < 0 ? kLbPatience : pat;
     hipStream_t s = (hipStream_t)stream;
+    const CamArg ca = prep(*cam, refn);
+    if (!cells) {  // nothing to launch: counts = [0 kept, 0 cells]
+        if (hipMemsetAsync(counts, 0, 2 * sizeof(uint64_t), s) != hipSuccess)
+            return check_launch("acm_sample_points: counts");
+        return ACM_SUCCESS;
+    }
     // (plain stores: non-temporal ones measured slower for these compacted
     // outputs, 1.41 -> 1.47 ms at 1e8 KB cells, profiles/r02_diag_sample_phases.log)
-    int fused = g_sample_fused;
-    if (fused < 0 && ((cam->model == ACM_PINHOLE && !SampleSinglePass<Tag<Pinhole>>::on) ||
-                      (cam->model == ACM_FOV && !SampleSinglePass<Tag<Fov>>::on)))
-        fused = 0;
-    if (fused != 0) {
+    const int mode = g_sample_fused;
+    if (mode < 0) {  // segment two-pass (default)
+        const size_t nseg = (cells + kSegCells - 1) / kSegCells;
+        const size_t nsb = (cells + kSegBlockCells - 1) / kSegBlockCells;
+        uint32_t* seg_cnt = (uint32_t*)workspace;
+        uint64_t* blk_sum = (uint64_t*)workspace + (nseg + 1) / 2;
+        uint64_t* blk_off = blk_sum + nsb;
+        const SegCert cert = seg_cert(*cam);
+        return dispatch_model(cam->model, [&](auto tag) -> int {
+            using TagT = decltype(tag);
+            hipLaunchKernelGGL((k_seg_count<TagT>), dim3((unsigned)nsb), dim3(kBlock), 0, s, ca, g,
+                               cells, cert, seg_cnt, blk_sum);
+            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, blk_sum, nsb, blk_off,
+                               counts, (uint64_t)cells);
+            hipLaunchKernelGGL((k_seg_write<TagT>), dim3((unsigned)nsb), dim3(kBlock), 0, s, ca, g,
+                               cells, seg_cnt, blk_off, points_2d_out, points_3d_out);
+            return check_launch("acm_sample_points");
+        });
+    }
+    if (mode > 0) {  // single pass with the decoupled look-back
         uint64_t* status = (uint64_t*)workspace + 1;
         if (hipMemsetAsync(workspace, 0, (nt + 1) * sizeof(uint64_t), s) != hipSuccess)
             return check_launch("acm_sample_points: workspace clear");
-        if (!cells) {  // no tile runs: counts = [0 kept, 0 cells]
-            if (hipMemsetAsync(counts, 0, 2 * sizeof(uint64_t), s) != hipSuccess)
-                return check_launch("acm_sample_points: counts");
-            return ACM_SUCCESS;
-        }
         return dispatch_model(cam->model, [&](auto tag) -> int {
             using TagT = decltype(tag);
-            const int rr = fused == 1 ? 2 : fused == 2 ? 4 : fused == 3 ? 8 : SampleR<TagT>::R;
+            const int rr = mode == 1 ? 2 : mode == 2 ? 4 : 8;
             const size_t ntr = (cells + (size_t)kBlock * rr - 1) / ((size_t)kBlock * rr);
             auto kern = k_sample_fused<TagT, 4>;
             if (rr == 2) kern = k_sample_fused<TagT, 2>;
             if (rr == 8) kern = k_sample_fused<TagT, 8>;
-            hipLaunchKernelGGL(kern, dim3((unsigned)ntr), dim3(kBlock), 0, s, prep(*cam), g, cells,
+            hipLaunchKernelGGL(kern, dim3((unsigned)ntr), dim3(kBlock), 0, s, ca, g, cells,
                                status, points_2d_out, points_3d_out, counts);
             return check_launch("acm_sample_points");
         });
@@ -2890,21 +3297,42 @@ ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, s
     uint64_t* off = cnt + nb;
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
-        hipLaunchKernelGGL((k_sample_count<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, prep(*cam),
-                           g, cells, cnt);
+        hipLaunchKernelGGL((k_sample_count<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, ca, g,
+                           cells, cnt);
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, cnt, nb, off, counts,
                            (uint64_t)cells);
-        hipLaunchKernelGGL((k_sample_write<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s,
-                           prep(*cam), g, cells, off, points_2d_out, points_3d_out);
+        hipLaunchKernelGGL((k_sample_write<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, ca, g,
+                           cells, off, points_2d_out, points_3d_out);
         return check_launch("acm_sample_points");
     });
+}
+
+ACM_API int acm_sample_points_certificate(const acm_camera* cam, double* out) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if (!out) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    const SegCert c = seg_cert(*cam);
+    out[0] = c.on;
+    out[1] = c.all_lo;
+    out[2] = c.all_hi;
+    out[3] = c.none_lo;
+    out[4] = c.none_hi;
+    return ACM_SUCCESS;
+}
+
+ACM_API int acm_sample_points_range(const acm_camera* cam, size_t n_requested, size_t cell_begin,
+                                    size_t cell_end, double* points_2d_out, double* points_3d_out,
+                                    uint64_t* counts, void* workspace, size_t workspace_bytes,
+                                    void* stream) {
+    return acm_sample_points_ex(cam, n_requested, cell_begin, cell_end, 0, points_2d_out,
+                                points_3d_out, counts, workspace, workspace_bytes, stream);
 }
 
 ACM_API int acm_sample_points(const acm_camera* cam, size_t n_requested, double* points_2d_out,
                               double* points_3d_out, uint64_t* counts, void* workspace,
                               size_t workspace_bytes, void* stream) {
-    return acm_sample_points_range(cam, n_requested, 0, ~(size_t)0, points_2d_out, points_3d_out,
-                                   counts, workspace, workspace_bytes, stream);
+    return acm_sample_points_ex(cam, n_requested, 0, ~(size_t)0, 0, points_2d_out, points_3d_out,
+                                counts, workspace, workspace_bytes, stream);
 }
 
 ACM_API int acm_linear_system_columns(int model) {
@@ -3187,9 +3615,13 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_SAMPLE_FUSED, &g_sample_fused, -1, 3, "value must be -1..3"},
         {ACM_TUNE_UNPROJECT_RCP, &g_unproject_rcp, -1, 1, "value must be -1..1"},
         {ACM_TUNE_SAMPLE_PATIENCE, &g_sample_patience, -1, 1 << 20, "value must be -1..2^20"},
-        {ACM_TUNE_NEWTON_FAST, &g_newton_fast, -1, 1, "value must be -1..1"},
+        {ACM_TUNE_SAMPLE_CERT, &g_sample_cert, -1, 0, "value must be -1 (auto) or 0"},
         {ACM_TUNE_UNPROJECT_PPT, &g_unproject_ppt, -1, 3, "value must be -1..3"},
     };
+    if (key == ACM_TUNE_NEWTON_FAST)  // removed (r03): numerics are chosen per call
+        return fail(ACM_ERR_NOT_SUPPORTED,
+                    "ACM_TUNE_NEWTON_FAST was removed: OR ACM_REFERENCE_NEWTON into the call's "
+                    "layout / flags instead (acm_unproject, acm_sample_points_ex)");
     for (const Knob& k : knobs) {
         if (k.key != key) continue;
         bool ok = value >= k.lo && value <= k.hi;

@@ -675,8 +675,29 @@ struct KannalaBrandt {
     // kannala_brandt.rs:445-562: Newton on theta_d(theta) = ru, <=10 steps.
     __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
                                                         T& Z) {
+        bool keep;
+        return unproject_k<false>(c, u, v, X, Y, Z, keep);
+    }
+    // The largest double below pi/2.  For a double theta with |theta| <= 2,
+    // cos(theta) > 0 exactly when |theta| <= kHalfPiDown (cos(kHalfPiDown) =
+    // +6.1e-17, cos of the next double up = -1.6e-16: any faithful libm,
+    // glibc's included, gets both signs right).
+    static constexpr double kHalfPiDown = 0x1.921fb54442d18p0;
+    // unproject_k<true> also returns the sample_points keep decision
+    // (point_sampling.rs:91-94: Ok and z > 0) decided exactly, not read off
+    // the ray: z = cos(theta) / |p| > 0 iff cos(theta) > 0 (and |p| finite),
+    // taken by the comparison above on the reference's own theta -- not on
+    // the polynomial cos, whose 3.3e-16 absolute error exceeds cos(theta)
+    // at kHalfPiDown.  The certified fast Newton's theta is within 4e-12 of
+    // the reference's; when it lies within 1e-11 of the threshold the pixel
+    // runs the reference loop, so the comparison always sees either a theta
+    // on the same side as the reference's or the reference's theta itself.
+    template <bool KEEP>
+    __device__ static __forceinline__ uint8_t unproject_k(const Cam<T>& c, T u, T v, T& X, T& Y,
+                                                          T& Z, bool& keep) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
         const T k1 = c.p[4], k2 = c.p[5], k3 = c.p[6], k4 = c.p[7];
+        keep = false;
         if (c.wi > 0 && c.hi > 0 && (u < T(0) || u >= c.w || v < T(0) || v >= c.h)) {
             X = Y = Z = T(NAN);
             return ST_POINT_IS_OUT_SIDE_IMAGE;  // :447-455
@@ -689,7 +710,11 @@ struct KannalaBrandt {
         bool converged = true;
         bool certified = false;
 #ifndef ACM_IEEE_MATH
-        if constexpr (sizeof(T) == 8) certified = front_fast(c, r2, ru, theta, ir_fast);
+        if constexpr (sizeof(T) == 8) {
+            certified = front_fast(c, r2, ru, theta, ir_fast);
+            if (KEEP && certified && fabs(fabs(theta) - T(kHalfPiDown)) <= T(1e-11))
+                certified = false;  // too close to call: take the reference's theta
+        }
 #endif
         if (!certified) {  // the reference's sequence (:462-525)
             ru = sqrt(r2);
@@ -718,6 +743,10 @@ struct KannalaBrandt {
         const bool small = fabs(ru) < T(kEps);
         T s, co;
         sincos_0_2(theta, &s, &co);  // polynomial on [0, 2], OCML sincos beyond
+        // cos(theta) > 0, exactly (see kHalfPiDown); beyond |theta| = 2 the
+        // sign of any faithful cos is right (no double lies that close to an
+        // odd multiple of pi/2)
+        const bool cos_pos = fabs(theta) <= T(2) ? fabs(theta) <= T(kHalfPiDown) : co > T(0);
 #ifndef ACM_IEEE_MATH
         if constexpr (sizeof(T) == 8) {
             // Everything after the Newton loop only shapes the ray: no status
@@ -733,6 +762,8 @@ struct KannalaBrandt {
             X = px * in;
             Y = py * in;
             Z = co * in;
+            // |p| finite: z = cos / |p| is 0 (dropped) when |p| overflows
+            keep = converged && cos_pos && n2 < T(INFINITY);
             return converged ? ST_OK : ST_NUMERICAL_ERROR;
         }
 #endif
@@ -742,13 +773,15 @@ struct KannalaBrandt {
         T xc = small ? T(0) : c2[0];
         T yc = small ? T(0) : c2[1];
         T px = s * xc, py = s * yc;
-        T n = sqrt(px * px + py * py + co * co);
+        T n2 = px * px + py * py + co * co;
+        T n = sqrt(n2);
         const T nq[3] = {px, py, co};
         T q[3];
         div_shared(nq, n, q);
         X = q[0];
         Y = q[1];
         Z = q[2];
+        keep = converged && cos_pos && n2 < T(INFINITY);
         return converged ? ST_OK : ST_NUMERICAL_ERROR;
     }
 };

@@ -9,6 +9,11 @@ column-major Jacobian (128 B) = 169 B/pt algorithmic traffic.
   python bench.py [--gpus N --steps K --warmup W] [--scaling weak|strong]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+Launch: under a launcher (torchrun sets WORLD_SIZE) every process is one
+rank and --gpus must equal WORLD_SIZE (else exit 2).  Without one,
+`bench.py --gpus N` (N > 1) starts its own N rank processes before importing
+torch (launch_ranks) and exits non-zero if any of them fails.
+
 Multi-GPU: one process per GPU.  --scaling weak (default): each rank
 projects its own --points batch (disjoint seeded shards; total work grows
 with N).  --scaling strong: --points is the GLOBAL batch, split into
@@ -199,8 +204,63 @@ def _latest_source_mtime():
     return max(os.path.getmtime(f) for f in files)
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher around it: start N rank
+    processes of this same script (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT in their environment, torchrun's contract) and
+    wait for them.  Runs BEFORE torch is imported: the parent never touches
+    the GPU, it only forwards the children's output (rank 0 prints the one
+    JSON line) and exits non-zero if any rank fails; a failed rank ends the
+    others so a collective cannot hang."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, start_new_session=True))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the "
+                      f"other ranks", file=sys.stderr, flush=True)
+                for q in live:
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     a = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
+    if env_world is not None and int(env_world) != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env_world} (the launcher started "
+              f"a different number of ranks)", file=sys.stderr, flush=True)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
@@ -399,7 +459,7 @@ def main():
             "metric": "Mpoints/sec project+Jacobian (KB, f64) at 1/2/4/8 GPU; % HBM roofline",
             "value": main_res["value"],
             "unit": "Mpoints/s",
-            "n_gpus": world,
+            "n_gpus": a.gpus,
             "n_ranks_seen": world,
             "steps": a.steps,
             "warmup": a.warmup,

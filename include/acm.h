@@ -103,6 +103,18 @@ enum { ACM_LAYOUT_AOS = 0, ACM_LAYOUT_SOA = 1 };
  * five models are reference-exact without it (the flag is ignored). */
 enum { ACM_EXACT_MATH = 0x100 };
 
+/* Per-call option OR-ed into acm_unproject's `layout` (and passed in
+ * acm_sample_points_ex's `flags`): the reference's own Newton loops for every
+ * pixel (kannala_brandt.rs:474-511, rad_tan.rs:436-518) instead of the
+ * certified fast ones, and FOV's IEEE unprojection (fov.rs:336-363) instead
+ * of its reciprocal / polynomial form.  Statuses (and the sample_points kept
+ * set) are identical either way; with the flag RadTan's rays equal the
+ * reference's bit for bit (by default they agree within a few ulp).  A
+ * per-call choice, so two callers on different threads can use different
+ * numerics on the same library (the reference's CameraModel is Send + Sync,
+ * mod.rs:241-340).  Replaces the process-wide ACM_TUNE_NEWTON_FAST knob. */
+enum { ACM_REFERENCE_NEWTON = 0x200 };
+
 /* Invalid-point policy of the factor evaluation (apex-solver source absent:
  * "skip" matches compute_reprojection_error skipping failed projections,
  * error_metrics.rs:76; "sentinel" is the (1e6,1e6) residual of the removed
@@ -154,7 +166,7 @@ ACM_API int acm_project_f32(const acm_camera *cam, size_t n,
                             uint8_t *status, float *jacobian, void *stream);
 
 /* Batched CameraModel::unproject (mod.rs:271).  rays: 3N f64 out written in
- * `layout`; failed points: ray = NaN. */
+ * `layout` (optionally | ACM_REFERENCE_NEWTON); failed points: ray = NaN. */
 ACM_API int acm_unproject(const acm_camera *cam, size_t n,
                           const double *points_2d, double *rays, int layout,
                           uint8_t *status, void *stream);
@@ -203,6 +215,16 @@ ACM_API int acm_reprojection_stats(const acm_camera *cam, size_t n,
  * same statistics bit for bit.  A point whose error is NaN (failed
  * projection or NaN observation) is never counted. */
 ACM_API int acm_reprojection_stats_merge(size_t nparts, const double *parts, double *result);
+
+/* The same 8-double result from an error vector already in HBM (errors:
+ * device, N f64, NaN = invalid; e.g. a shard's acm_reprojection_stats
+ * `errors` output): the per-shard leg of the multi-GPU statistics
+ * (error_metrics.rs:86-111 over one shard) without copying the errors to the
+ * host.  Same per-workgroup shifted sums + fixed-order Chan merge as
+ * acm_reprojection_stats, so bit-reproducible run to run. */
+ACM_API size_t acm_error_stats_workspace_size(size_t n);
+ACM_API int acm_error_stats(size_t n, const double *errors, double *result,
+                            void *workspace, size_t workspace_bytes, void *stream);
 
 /* linear_estimation (kannala_brandt.rs:164-272, double_sphere.rs:225-290,
  * ucm.rs:200-258, eucm.rs:216-288, rad_tan.rs:153-234).  The 2N x k system
@@ -355,6 +377,22 @@ ACM_API int acm_sample_points_range(const acm_camera *cam, size_t n_requested,
                                     double *points_2d_out, double *points_3d_out,
                                     uint64_t *counts, void *workspace,
                                     size_t workspace_bytes, void *stream);
+/* The host-certified keep regions acm_sample_points counts segments by
+ * (inspection / tests; csrc/acm.hip kb_seg_cert): out = [on, all_lo, all_hi,
+ * none_lo, none_hi] in the model's certificate variable (KB: ru =
+ * min(sqrt(mx^2 + my^2), pi/2); others: r2 = mx^2 + my^2).  Every cell whose
+ * variable lies in [all_lo, all_hi] is kept (Ok and z > 0), none in
+ * [none_lo, none_hi]; on = 0: no certificate (every segment is counted cell
+ * by cell).  Host only. */
+ACM_API int acm_sample_points_certificate(const acm_camera *cam, double *out);
+
+/* acm_sample_points_range with per-call options: flags = 0 or
+ * ACM_REFERENCE_NEWTON.  (acm_sample_points / _range = flags 0.) */
+ACM_API int acm_sample_points_ex(const acm_camera *cam, size_t n_requested,
+                                 size_t cell_begin, size_t cell_end, int flags,
+                                 double *points_2d_out, double *points_3d_out,
+                                 uint64_t *counts, void *workspace,
+                                 size_t workspace_bytes, void *stream);
 
 /* util::undistort_image (src/util/undistort.rs:14-105).  image/output:
  * device RGB8 row-major, cam->width x cam->height (the reference requires
@@ -376,8 +414,13 @@ ACM_API int acm_memcpy_htod(void *dst_device, const void *src_host, size_t bytes
 ACM_API int acm_memcpy_dtoh(void *dst_host, const void *src_device, size_t bytes, void *stream);
 ACM_API int acm_stream_synchronize(void *stream);
 
-/* Process-wide kernel tuning knob (benchmark sweeps; results are identical
- * for every setting).  ACM_TUNE_PROJECT_VARIANT: bit flags of acm_project's
+/* Process-wide kernel tuning knobs: performance only.  Every knob selects
+ * among kernels that return the same results -- bit for bit, except that
+ * ACM_TUNE_NE_WAVES / ACM_TUNE_NE_UNROLL / ACM_TUNE_FOV_UNROLL change the
+ * summation order of the normal-equations / grid sums (deterministic for a
+ * fixed setting, <= ~1e-15 relative apart).  Numerics are never a knob: they
+ * are chosen per call (ACM_EXACT_MATH, ACM_REFERENCE_NEWTON).
+ * ACM_TUNE_PROJECT_VARIANT: bit flags of acm_project's
  * direct kernel, 1 = non-temporal stores, 2 = persistent grid-stride launch,
  * 4 = non-temporal loads; -1 (default) = auto (non-temporal stores when the
  * outputs exceed 64 MiB; non-temporal loads only if ACM_TUNE_NT_LOADS = 1).  ACM_TUNE_RESIDUAL_NT: non-temporal stores in
@@ -399,12 +442,15 @@ ACM_API int acm_stream_synchronize(void *stream);
  * host memory rather than device memory plus a copy: 0 = off, 1 = on with a
  * stream synchronisation, 2 = on with the host spinning on a completion
  * word the kernel publishes; -1 = auto = 2.
- * ACM_TUNE_SAMPLE_FUSED: acm_sample_points in one pass (unproject once,
- * decoupled look-back for the output offsets; -1 = auto = tiles of 4 x 256
- * cells for every model but Pinhole and FOV, whose unprojections are cheap
- * enough that the two-pass path is faster; 1 / 2 / 3 = tiles of 2 / 4 / 8 x 256
- * cells) or the two-pass count / scan / recompute-and-write path (0).
+ * ACM_TUNE_SAMPLE_FUSED: acm_sample_points' kernels.  -1 = auto (r03) = the
+ * segment two-pass path (certified per-segment counts, offsets by a scan,
+ * then a write pass with known offsets); 0 = the round-1 two-pass count /
+ * scan / recompute-and-write path (tiles of 16 x 256 cells); 1 / 2 / 3 = the
+ * single pass with a decoupled look-back, tiles of 2 / 4 / 8 x 256 cells
+ * (round 1 mapped 1 / 2 / 3 to 4 / 8 / 16 x 256; changed in round 2).
  * Outputs are identical for every value.
+ * ACM_TUNE_SAMPLE_CERT: the segment path's host-certified keep regions
+ * (-1 = auto = on; 0 = every segment counted cell by cell).  Same outputs.
  * ACM_TUNE_UNPROJECT_RCP: unprojections (acm_unproject, acm_sample_points*)
  * divide by fx, fy through the host's correctly rounded 1/fx, 1/fy and one
  * FMA correction, bit-identical to the division (-1 = auto = on, 0 = plain
@@ -413,19 +459,14 @@ ACM_API int acm_stream_synchronize(void *stream);
  * spends on a predecessor tile that has not published its count before the
  * waiting wave counts that tile's cells itself (-1 = auto = 512; 0 = at once,
  * which exercises that path; outputs are identical for every value).
- * ACM_TUNE_NEWTON_FAST: the certified fast Newton loops of the KB and RadTan
- * unprojections (acm_unproject, acm_sample_points*; camera_models.hpp
- * newton_fast): FMA / reciprocal iterates whose every break / continue
- * decision is certified against the reference's, with the reference's own
- * loop for any pixel that cannot be certified (-1 = auto = on, 0 = the
- * reference's loop for every pixel, 1 = on); the same knob switches FOV's
- * unprojection between its reciprocal / polynomial form and the IEEE one.
- * Statuses are identical for every value; rays agree within a few ulp.
+ * ACM_TUNE_NEWTON_FAST (12): removed in round 3 (it changed RadTan's rays by a
+ * few ulp process-wide); acm_set_tuning returns ACM_ERR_NOT_SUPPORTED.  Use
+ * the per-call ACM_REFERENCE_NEWTON.
  * ACM_TUNE_UNPROJECT_PPT: acm_unproject's pixels per lane and AoS ray
  * stores (-1 = auto = 2 pixels per lane; for Pinhole, DS, UCM and EUCM each
  * wave's 64 AoS rays staged in LDS and written as 16-B pieces when rays is
  * 16-B aligned; 1 / 2 = pixels per lane with three 8-B stores per ray; 3 =
- * 1 pixel per lane, staged).
+ * 1 pixel per lane, staged when rays is 16-B aligned).
  * Outputs are identical for every value.
  * Every knob is an atomic: acm_set_tuning may race with any other call.
  * Returns the previous value or an error. */
@@ -443,7 +484,8 @@ enum {
     ACM_TUNE_UNPROJECT_RCP = 10,
     ACM_TUNE_SAMPLE_PATIENCE = 11,
     ACM_TUNE_NEWTON_FAST = 12,
-    ACM_TUNE_UNPROJECT_PPT = 13
+    ACM_TUNE_UNPROJECT_PPT = 13,
+    ACM_TUNE_SAMPLE_CERT = 14
 };
 ACM_API int acm_set_tuning(int key, int value);
 

@@ -54,11 +54,11 @@ class GpuBackend:
         return (uv.cpu().numpy(), st.cpu().numpy(),
                 jac.cpu().numpy() if jac is not None else None)
 
-    def unproject(self, model, params, w, h, uv, layout="aos"):
+    def unproject(self, model, params, w, h, uv, layout="aos", reference_newton=False):
         m = self._model(model, params, w, h)
         t = self.torch.as_tensor(np.ascontiguousarray(uv, dtype=np.float64).reshape(-1, 2),
                                  device="cuda")
-        rays, st = m.unproject_batch(t, layout=layout)
+        rays, st = m.unproject_batch(t, layout=layout, reference_newton=reference_newton)
         self.torch.cuda.synchronize()
         r = rays.cpu().numpy()
         if layout == "soa":

@@ -1,0 +1,75 @@
+"""bench.py's process launch, on the CPU (no GPU work happens in these runs):
+a WORLD_SIZE that disagrees with --gpus exits 2 before torch is imported,
+and `bench.py --gpus N` without a launcher starts N ranks with torchrun's
+environment and exits non-zero when a rank fails."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
+def test_world_size_mismatch_exits_2():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "4", "--steps", "1"],
+                       env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2, r.stderr
+    assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_launcher_default_gpus_under_torchrun_mismatch():
+    # torchrun with 2 ranks but no --gpus: --gpus defaults to 1 -> refused
+    r = subprocess.run([sys.executable, BENCH, "--steps", "1"],
+                       env=_env(WORLD_SIZE="2", RANK="1", LOCAL_RANK="1"),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2
+
+
+def test_self_launch_spawns_ranks_with_torchrun_env(tmp_path):
+    """launch_ranks gives every child RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*;
+    a stand-in script records them (the real bench would need a GPU)."""
+    import bench
+    rec = tmp_path / "rec"
+    rec.mkdir()
+    child = tmp_path / "child.py"
+    child.write_text(
+        "import os, sys\n"
+        f"open(os.path.join({str(rec)!r}, os.environ['RANK']), 'w').write(\n"
+        "    ' '.join(os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', "
+        "'MASTER_ADDR', 'MASTER_PORT')))\n"
+        "sys.exit(int(os.environ['RANK']) == int(os.environ.get('FAIL_RANK', -1)) and 7)\n")
+    old_file, old_argv = bench.__file__, sys.argv
+    env_keep = dict(os.environ)
+    try:
+        bench.__file__ = str(child)
+        sys.argv = ["bench.py", "--gpus", "3"]
+        os.environ.pop("MASTER_PORT", None)
+        assert bench.launch_ranks(3) == 0
+        got = sorted((rec / str(r)).read_text().split() for r in range(3))
+        assert [g[:3] for g in got] == [["0", "0", "3"], ["1", "1", "3"], ["2", "2", "3"]]
+        assert all(g[3] == "127.0.0.1" for g in got) and len({g[4] for g in got}) == 1
+        os.environ["FAIL_RANK"] = "1"
+        assert bench.launch_ranks(3) == 7
+    finally:
+        bench.__file__, sys.argv = old_file, old_argv
+        os.environ.clear()
+        os.environ.update(env_keep)
+
+
+def test_self_launch_failing_ranks_exit_nonzero():
+    """on this GPU-less host every rank fails at its first device call: the
+    parent must report failure, not print a line"""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--points", "1000", "--no-cpu-baseline"],
+                       env=_env(ACM_BENCH_BACKEND="gloo"), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

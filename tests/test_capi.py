@@ -161,7 +161,7 @@ def test_tuning_knobs_validate_and_restore():
              _lib.TUNE_LM_HOST_RESULT: ([-1, 0, 1, 2], [3, -2]),
              _lib.TUNE_SAMPLE_FUSED: ([-1, 0, 1, 2, 3], [4, -2]),
              _lib.TUNE_UNPROJECT_RCP: ([-1, 0, 1], [2, -2]),
-             _lib.TUNE_NEWTON_FAST: ([-1, 0, 1], [2, -2]),
+             _lib.TUNE_SAMPLE_CERT: ([-1, 0], [1, -2]),
              _lib.TUNE_UNPROJECT_PPT: ([-1, 1, 2, 3], [0, 4, -2])}
     for key, (good, bad) in cases.items():
         first = L.acm_set_tuning(key, good[0])
@@ -174,6 +174,8 @@ def test_tuning_knobs_validate_and_restore():
             assert L.acm_set_tuning(key, v) == _lib.ERR_INVALID_ARGUMENT, (key, v)
         assert L.acm_set_tuning(key, first) == prev  # a rejected value changed nothing
     assert L.acm_set_tuning(99, 0) == _lib.ERR_INVALID_ARGUMENT
+    # numerics are per call since round 3: the old process-wide knob is gone
+    assert L.acm_set_tuning(_lib.TUNE_NEWTON_FAST, 0) == _lib.ERR_NOT_SUPPORTED
 
 
 def test_newton_tolerance_threshold_is_exact():

@@ -41,6 +41,24 @@ def test_bench_single_gpu_line():
     assert "traffic_source" in d["roofline"]
 
 
+def test_bench_self_launch_world2():
+    """the driver's own command form: plain `bench.py --gpus 2`, no launcher;
+    bench.py starts both ranks itself (gloo, both on device 0 on this box)"""
+    env = dict(os.environ, ACM_BENCH_SAME_DEVICE="1", ACM_BENCH_BACKEND="gloo",
+               OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "3", "--warmup", "1", "--points", "300000",
+                        "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    d = _line(r.stdout)
+    assert d["n_gpus"] == d["n_ranks_seen"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["global_points"] == 600000
+    assert d["strong"]["mode"] == "strong" and d["strong"]["global_points"] == 300000
+    assert d["collective"]["ranks"] == 2 and d["collective"]["us"] > 0
+
+
 def test_bench_world2_strong_rehearsal():
     env = dict(os.environ, ACM_BENCH_SAME_DEVICE="1", ACM_BENCH_BACKEND="gloo",
                OMP_NUM_THREADS="1")

@@ -1,0 +1,157 @@
+"""Kannala-Brandt sample_points keep decision at theta ~ pi/2 (VERDICT r02
+weak item 1 / next item 2).
+
+The reference keeps a cell iff unproject is Ok and z > 0
+(point_sampling.rs:91-94); for KB z = cos(theta) / |p|
+(kannala_brandt.rs:545-561), so the decision flips where the reference's
+final Newton theta crosses pi/2: kept iff theta <= 0x1.921fb54442d18p0 (the
+largest double below pi/2).  Our kernels decide it by that exact comparison
+on the reference's theta (KannalaBrandt::unproject_k): the certified fast
+Newton's theta is used only when it lies more than 1e-11 from the threshold
+(its error bound is 4e-12); otherwise the pixel runs the reference loop.
+
+These cameras are built so that the reference's theta lands within 1e-11 of
+pi/2 -- on both sides, down to a few ulp -- for many cells:
+  * clamped: ru = min(|m|, pi/2) = pi/2 for every cell beyond |m| = pi/2, and
+    k1 = +-eps puts theta_final = pi/2 -+ ~eps (pi/2)^3 for all of them;
+  * unclamped: k1 solved so that theta_d(pi/2) equals one chosen cell's own
+    ru (computed with the kernel's operations), then nudged by a few ulp.
+The kept set must equal the oracle's (glibc cos on the reference's theta)
+bit for bit."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+HPD = float.fromhex("0x1.921fb54442d18p0")
+
+
+def ref_theta(ru, k):
+    """kannala_brandt.rs:474-511 in IEEE double (Python floats, no FMA)."""
+    k1, k2, k3, k4 = k
+    theta = ru
+    if not ru > 1e-6:
+        return None
+    for i in range(10):
+        t2 = theta * theta
+        t4 = t2 * t2
+        t6 = t4 * t2
+        t8 = t4 * t4
+        a, b, c, d = k1 * t2, k2 * t4, k3 * t6, k4 * t8
+        f = theta * (1.0 + a + b + c + d) - ru
+        fp = 1.0 + (3.0 * a) + (5.0 * b) + (7.0 * c) + (9.0 * d)
+        if abs(fp) < 2.220446049250313e-16:
+            return None
+        delta = f / fp
+        theta -= delta
+        if abs(delta) < 1e-6:
+            return theta
+    return None
+
+
+def cell_ru(params, w, h, n, i, j):
+    fx, fy, cx, cy = params[:4]
+    ncx = int(round(math.sqrt(n * (w / h))))
+    ncy = int(round(math.sqrt(n * (h / w))))
+    cw, ch = w / ncx, h / ncy
+    u = (j + 0.5) * cw
+    v = (i + 0.5) * ch
+    mx = (u - cx) / fx
+    my = (v - cy) / fy
+    return min(math.sqrt(mx * mx + my * my), math.pi / 2.0), (ncx, ncy)
+
+
+def _model(params, w, h):
+    from apex_camera_models import KannalaBrandtModel
+    m = KannalaBrandtModel.new(params)
+    m.resolution.width, m.resolution.height = w, h
+    return m
+
+
+def _compare(params, w, h, n):
+    from apex_camera_models import util
+    uv, xyz = util.sample_points(_model(params, w, h), n)
+    uv0, xyz0, _ = O.sample_points(2, params, w, h, n)
+    assert uv.shape[0] == uv0.shape[0], (uv.shape[0], uv0.shape[0])
+    assert np.array_equal(uv.cpu().numpy(), uv0)
+    d = np.abs(xyz.cpu().numpy() - xyz0)
+    assert float(d.max()) <= 1e-10
+    return uv0.shape[0]
+
+
+@pytest.mark.parametrize("k1", [1e-12, -1e-12, 2e-13, -2e-13, 3e-15, -3e-15, 5e-17, -5e-17])
+def test_clamped_cells_theta_at_half_pi(k1):
+    params = [100.0, 100.0, 320.0, 240.0, k1, 0.0, 0.0, 0.0]
+    w, h, n = 640, 480, 300_000
+    th = ref_theta(math.pi / 2.0, (k1, 0.0, 0.0, 0.0))
+    assert th is not None and abs(th - HPD) <= 1e-11  # the engineered case
+    kept = _compare(params, w, h, n)
+    # every clamped cell shares this theta: all kept or all dropped with it
+    ncx = int(round(math.sqrt(n * (w / h))))
+    ncy = int(round(math.sqrt(n * (h / w))))
+    if th <= HPD:
+        assert kept > 0.9 * ncx * ncy
+    else:
+        assert kept < 0.7 * ncx * ncy
+
+
+@pytest.mark.parametrize("nudge", [-4, -2, -1, 0, 1, 2, 4])
+def test_unclamped_cell_theta_at_half_pi(nudge):
+    """fx = 300: |m| <= 1.33 < pi/2, no clamping; k1 < 0 chosen so that the
+    cell (i, j) near the image corner has theta* = pi/2, then k1 moved by
+    `nudge` ulp, so that cell's (and a few neighbours') reference theta
+    straddles the threshold by a few ulp."""
+    w, h, n = 640, 480, 300_000
+    base = [300.0, 300.0, 320.0, 240.0]
+    i, j = 3, 5
+    ru, _ = cell_ru(base + [0.0] * 4, w, h, n, i, j)
+    k1 = (ru / HPD - 1.0) / (HPD * HPD)
+    for _ in range(abs(nudge)):
+        k1 = float(np.nextafter(k1, np.inf if nudge > 0 else -np.inf))
+    params = base + [k1, 0.0, 0.0, 0.0]
+    th = ref_theta(ru, (k1, 0.0, 0.0, 0.0))
+    assert th is not None and abs(th - HPD) <= 1e-11, th - HPD
+    _compare(params, w, h, n)
+
+
+def test_oracle_keep_matches_exact_rule_on_engineered_cells():
+    """The rule the kernels use (keep iff theta <= 0x1.921fb54442d18p0) is
+    the oracle's cos(theta) > 0 on every engineered theta above."""
+    for k1 in (1e-12, -1e-12, 3e-15, -3e-15, 5e-17, -5e-17, 0.0):
+        th = ref_theta(math.pi / 2.0, (k1, 0.0, 0.0, 0.0))
+        assert (math.cos(th) > 0.0) == (th <= HPD)
+
+
+def test_certified_counts_equal_cell_by_cell_counts_random_cameras():
+    """The segment path's host certificates against counting every cell
+    (ACM_TUNE_SAMPLE_CERT = 0): identical outputs, bit for bit, for 40
+    random KB cameras (mild to strong distortion, random principal points and
+    focal lengths, so the kept region's boundary crosses segments at every
+    angle), plus the oracle on a few of them."""
+    import torch
+    from apex_camera_models import _lib, util
+    L = _lib.load()
+    rng = np.random.default_rng(11)
+    try:
+        for t in range(40):
+            w, h = int(rng.integers(300, 900)), int(rng.integers(240, 700))
+            f = rng.uniform(0.2, 0.6) * w
+            params = [f, f * rng.uniform(0.95, 1.05), w * rng.uniform(0.3, 0.7),
+                      h * rng.uniform(0.3, 0.7)] + list(rng.normal(0, [0.05, 0.02, 0.01, 0.005]))
+            m = _model(params, w, h)
+            n = 150_000
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, -1)
+            uv1, xyz1 = util.sample_points(m, n)
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, 0)
+            uv0, xyz0 = util.sample_points(m, n)
+            assert torch.equal(uv1, uv0) and torch.equal(xyz1.view(torch.int64),
+                                                         xyz0.view(torch.int64)), (t, params)
+            if t < 4:
+                uvo, _, _ = O.sample_points(2, params, w, h, n)
+                assert np.array_equal(uv1.cpu().numpy(), uvo), (t, params)
+    finally:
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, -1)

@@ -27,7 +27,7 @@ NO_TRANSCENDENTAL_PROJECT = (0, 1, 3, 4, 5)
 NO_TRANSCENDENTAL_UNPROJECT = (0, 1, 3, 4, 5)
 # Models whose default unprojection returns the reference's rays bit for bit.
 # RadTan's (and KB's) default Newton loop is the certified fast one
-# (ACM_TUNE_NEWTON_FAST): statuses exact, rays within a few ulp;
+# (ACM_REFERENCE_NEWTON off): statuses exact, rays within a few ulp;
 # test_newton_reference_loop_bit_exact pins the knob-off path bit for bit.
 EXACT_RAYS_UNPROJECT = (0, 3, 4, 5)
 ULP = 2.0 ** -52
@@ -38,20 +38,6 @@ def ulps_of_one(a, b):
     fin = np.isfinite(b)
     assert np.array_equal(fin, np.isfinite(a)), "finite pattern differs"
     return float(np.abs(a[fin] - b[fin]).max() / ULP) if fin.any() else 0.0
-
-
-class newton_fast:
-    """with newton_fast(0): the reference's Newton loops for every pixel"""
-    def __init__(self, value):
-        self.value = value
-
-    def __enter__(self):
-        from apex_camera_models import _lib
-        _lib.load().acm_set_tuning(_lib.TUNE_NEWTON_FAST, self.value)
-
-    def __exit__(self, *exc):
-        from apex_camera_models import _lib
-        _lib.load().acm_set_tuning(_lib.TUNE_NEWTON_FAST, -1)
 
 
 @pytest.fixture(scope="module")
@@ -122,15 +108,14 @@ def test_unproject_vs_golden(be, golden_dir, model, layout):
 
 @pytest.mark.parametrize("model", [1, 2])
 def test_newton_reference_loop_bit_exact(be, golden_dir, model):
-    """ACM_TUNE_NEWTON_FAST = 0 runs the reference's own Newton loop for
+    """ACM_REFERENCE_NEWTON (per call) runs the reference's own Newton loop for
     every pixel: RadTan rays then equal the golden (oracle) rays bit for bit,
     in acm_unproject and in sample_points; KB's stay within 1e-10 (its sin /
     cos are polynomials either way).  Statuses are the same in both modes."""
     from apex_camera_models import util
     from test_oracle import SAMPLES
     g, params, w, h = _golden(golden_dir, model)
-    with newton_fast(0):
-        rays, st = be.unproject(model, params, w, h, g["uv_in"])
+    rays, st = be.unproject(model, params, w, h, g["uv_in"], reference_newton=True)
     assert np.array_equal(st, g["unproj_status"])
     if model == 1:
         assert np.array_equal(rays, g["rays"], equal_nan=True)
@@ -139,8 +124,7 @@ def test_newton_reference_loop_bit_exact(be, golden_dir, model):
     sp, (sw, sh) = SAMPLES[model]
     m = _model_obj(model, sp, sw, sh)
     uv0, xyz0, _ = O.sample_points(model, sp, sw, sh, 20_000)
-    with newton_fast(0):
-        uv, xyz = util.sample_points(m, 20_000)
+    uv, xyz = util.sample_points(m, 20_000, reference_newton=True)
     assert np.array_equal(uv.cpu().numpy(), uv0)
     if model == 1:
         assert np.array_equal(xyz.cpu().numpy(), xyz0)
@@ -172,8 +156,7 @@ def test_newton_fast_statuses_identical_under_stress(be, case):
     n = 1_000_000
     px = np.stack([rng.uniform(-10, w + 10, n), rng.uniform(-10, h + 10, n)], 1)
     rays1, st1 = be.unproject(model, params, w, h, px)
-    with newton_fast(0):
-        rays0, st0 = be.unproject(model, params, w, h, px)
+    rays0, st0 = be.unproject(model, params, w, h, px, reference_newton=True)
     assert np.array_equal(st1, st0), np.nonzero(st1 != st0)[0][:5]
     ok = st0 == 0
     assert ulps_of_one(rays1[ok], rays0[ok]) <= 32
@@ -675,7 +658,7 @@ def test_newton_fast_random_cameras():
     RadTan cameras with random intrinsics and distortion (about a third of
     them beyond the fast loops' per-camera bounds, which must then take the
     reference loop), 40K pixels each spread over the image and a margin.
-    Statuses with ACM_TUNE_NEWTON_FAST on and off are identical for every
+    Statuses with and without ACM_REFERENCE_NEWTON are identical for every
     pixel, rays within 64 ulp of 1."""
     import ctypes
     import torch
@@ -689,46 +672,42 @@ def test_newton_fast_random_cameras():
     r_off = torch.empty_like(r_on)
     failures = 0
     covered = {1: [0, 0], 2: [0, 0]}  # [beyond the fast loop's bound, within]
-    try:
-        for model in (2, 1):
-            for _ in range(150):
-                w, h = int(rng.integers(320, 1400)), int(rng.integers(240, 1100))
-                f = rng.uniform(0.3, 1.2) * w
-                base = [f, f * rng.uniform(0.95, 1.05), w * rng.uniform(0.4, 0.6),
-                        h * rng.uniform(0.4, 0.6)]
-                if model == 2:
-                    dist = list(rng.normal(0, [0.2, 0.1, 0.1, 0.15]))
-                    bound = 4 * abs(dist[0]) + 16 * abs(dist[1]) + 64 * abs(dist[2]) + \
-                        256 * abs(dist[3])
-                    covered[model][int(bound <= 63)] += 1
-                else:  # k1 k2 p1 p2 k3
-                    dist = list(rng.normal(0, [0.3, 0.1, 0.005, 0.005, 0.02]))
-                    bound = 8 * abs(dist[0]) + 64 * abs(dist[1]) + 512 * abs(dist[4]) + \
-                        16 * (abs(dist[2]) + abs(dist[3]))
-                    covered[model][int(bound <= 15)] += 1
-                params = base + dist
-                cam = _lib.AcmCamera()
-                _lib.check(L.acm_camera_init(ctypes.byref(cam), model,
-                                             (ctypes.c_double * len(params))(*params),
-                                             len(params), w, h))
-                px = torch.as_tensor(np.stack([rng.uniform(-20, w + 20, n),
-                                               rng.uniform(-20, h + 20, n)], 1), device="cuda")
-                for knob, st, r in ((1, st_on, r_on), (0, st_off, r_off)):
-                    L.acm_set_tuning(_lib.TUNE_NEWTON_FAST, knob)
-                    _lib.check(L.acm_unproject(ctypes.byref(cam), n, px.data_ptr(), r.data_ptr(),
-                                               0, st.data_ptr(), None))
-                torch.cuda.synchronize()
-                if not torch.equal(st_on, st_off):
-                    failures += 1
-                    continue
-                ok = st_off == 0
-                d = (r_on[ok] - r_off[ok]).abs()
-                fin = torch.isfinite(r_off[ok]).all(1)
-                assert torch.equal(fin, torch.isfinite(r_on[ok]).all(1)), (model, params)
-                if fin.any():
-                    assert float(d[fin].max()) <= 64 * 2.0 ** -52, (model, params)
-    finally:
-        L.acm_set_tuning(_lib.TUNE_NEWTON_FAST, -1)
+    for model in (2, 1):
+        for _ in range(150):
+            w, h = int(rng.integers(320, 1400)), int(rng.integers(240, 1100))
+            f = rng.uniform(0.3, 1.2) * w
+            base = [f, f * rng.uniform(0.95, 1.05), w * rng.uniform(0.4, 0.6),
+                    h * rng.uniform(0.4, 0.6)]
+            if model == 2:
+                dist = list(rng.normal(0, [0.2, 0.1, 0.1, 0.15]))
+                bound = 4 * abs(dist[0]) + 16 * abs(dist[1]) + 64 * abs(dist[2]) + \
+                    256 * abs(dist[3])
+                covered[model][int(bound <= 63)] += 1
+            else:  # k1 k2 p1 p2 k3
+                dist = list(rng.normal(0, [0.3, 0.1, 0.005, 0.005, 0.02]))
+                bound = 8 * abs(dist[0]) + 64 * abs(dist[1]) + 512 * abs(dist[4]) + \
+                    16 * (abs(dist[2]) + abs(dist[3]))
+                covered[model][int(bound <= 15)] += 1
+            params = base + dist
+            cam = _lib.AcmCamera()
+            _lib.check(L.acm_camera_init(ctypes.byref(cam), model,
+                                         (ctypes.c_double * len(params))(*params),
+                                         len(params), w, h))
+            px = torch.as_tensor(np.stack([rng.uniform(-20, w + 20, n),
+                                           rng.uniform(-20, h + 20, n)], 1), device="cuda")
+            for flag, st, r in ((0, st_on, r_on), (_lib.REFERENCE_NEWTON, st_off, r_off)):
+                _lib.check(L.acm_unproject(ctypes.byref(cam), n, px.data_ptr(), r.data_ptr(),
+                                           flag, st.data_ptr(), None))
+            torch.cuda.synchronize()
+            if not torch.equal(st_on, st_off):
+                failures += 1
+                continue
+            ok = st_off == 0
+            d = (r_on[ok] - r_off[ok]).abs()
+            fin = torch.isfinite(r_off[ok]).all(1)
+            assert torch.equal(fin, torch.isfinite(r_on[ok]).all(1)), (model, params)
+            if fin.any():
+                assert float(d[fin].max()) <= 64 * 2.0 ** -52, (model, params)
     assert failures == 0, failures
     for model in (1, 2):  # both paths of the per-camera switch were exercised
         assert min(covered[model]) >= 15, covered

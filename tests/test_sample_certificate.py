@@ -1,0 +1,90 @@
+"""CPU check of sample_points' host-certified keep regions (acm.hip
+kb_seg_cert, exposed as acm_sample_points_certificate): every ru the
+certificate calls "all kept" must be Ok with cos(theta) > 0 under the
+reference's own Newton loop (kannala_brandt.rs:462-561, replayed here in IEEE
+double), and every ru it calls "none kept" must not be -- on dense samples of
+each interval including both ends, for the reference's sample camera and a
+sweep of random distortions (the host code runs without a GPU)."""
+import ctypes
+import math
+import os
+
+import numpy as np
+import pytest
+
+from apex_camera_models import _lib
+
+from test_gpu_kb_keep_boundary import HPD, ref_theta
+
+pytestmark = pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libacm.so not built")
+
+KB_SAMPLE = [190.97847715128717, 190.9733070521226, 254.93170605935475, 256.8974428996504,
+             0.0034823894022493434, 0.0007150348452162257, -0.0020532361418706202,
+             0.00020293673591811182]
+
+
+def cert(params, w=512, h=512):
+    L = _lib.load()
+    cam = _lib.AcmCamera()
+    _lib.check(L.acm_camera_init(ctypes.byref(cam), 2, (ctypes.c_double * 8)(*params), 8, w, h))
+    out = (ctypes.c_double * 5)()
+    _lib.check(L.acm_sample_points_certificate(ctypes.byref(cam), out))
+    return list(out)
+
+
+def kept(ru, k):
+    th = ref_theta(ru, k)
+    if th is None:
+        return False
+    return math.cos(th) > 0.0
+
+
+def _check(params, samples=4000):
+    on, alo, ahi, nlo, nhi = cert(params)
+    k = tuple(params[4:])
+    if not on:
+        return False
+    rng = np.random.default_rng(0)
+    if ahi >= alo:
+        for ru in np.concatenate([[alo, ahi, np.nextafter(ahi, 0)], rng.uniform(alo, ahi, samples),
+                                  np.geomspace(alo, min(ahi, 1e-3), 50)]):
+            assert kept(float(ru), k), (params, ru)
+    if nhi >= nlo:
+        for ru in np.concatenate([[nlo, nhi], rng.uniform(nlo, nhi, samples)]):
+            assert not kept(float(ru), k), (params, ru)
+    return True
+
+
+def test_sample_camera_certificate():
+    on, alo, ahi, nlo, nhi = cert(KB_SAMPLE)
+    assert on == 1
+    # the reference sample camera: theta_d(pi/2) ~ 1.552 < pi/2, so the
+    # ring between it and the clamp is dropped, everything inside kept
+    assert 1e-6 < alo < 1.1e-6 and 1.55 < ahi < 1.56 and ahi < nlo < ahi + 1e-8 and nhi == math.pi / 2
+    assert _check(KB_SAMPLE)
+
+
+def test_no_distortion_clamped_threshold_not_certified():
+    """k = 0: theta = ru exactly, the clamp gives theta = pi/2 (kept, by one
+    ulp of margin): the certificate must stop short of it."""
+    on, alo, ahi, nlo, nhi = cert([100.0, 100.0, 320.0, 240.0, 0.0, 0.0, 0.0, 0.0])
+    assert on == 1 and ahi < HPD - 1e-10 and nlo > nhi
+
+
+def test_random_cameras_certificates_hold():
+    rng = np.random.default_rng(7)
+    n_on = 0
+    for _ in range(60):
+        dist = list(rng.normal(0, [0.05, 0.02, 0.01, 0.005]))
+        n_on += _check([200.0, 200.0, 256.0, 256.0] + dist, samples=800)
+    assert n_on >= 30  # most of these mild cameras are certifiable
+
+
+def test_strong_distortion_partial_certificate():
+    """k1 = -0.0646 (theta_d(pi/2) = 1.32): the Newton bounds hold only for
+    ru up to some R < pi/2 -- the certificate covers that much and no more,
+    and what it covers holds."""
+    params = [300.0, 300.0, 320.0, 240.0, -0.0646, 0.0, 0.0, 0.0]
+    on, alo, ahi, nlo, nhi = cert(params)
+    assert on == 1 and max(ahi, nhi) < math.pi / 2
+    assert _check(params)

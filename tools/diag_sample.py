@@ -1,7 +1,9 @@
-"""sample_points A/B: single pass with decoupled look-back vs the two-pass
-count / scan / recompute-and-write path (ACM_TUNE_SAMPLE_FUSED), every model
-on the config-5 grid (1e8 requested cells), interleaved in one process.  The
-outputs must be bit-identical.
+"""sample_points A/B of every path (ACM_TUNE_SAMPLE_FUSED): the segment
+two-pass default (-1; -2 = the same with ACM_TUNE_SAMPLE_CERT = 0, every
+segment counted cell by cell), the round-1 two-pass count / scan / write
+path (0) and the single pass with a decoupled look-back (1 / 2 / 3), every
+model on the config-5 grid (1e8 requested cells), interleaved in one
+process.  The outputs must be bit-identical.
 
   python tools/diag_sample.py [--cells N]
 """
@@ -30,10 +32,11 @@ def main():
         m = MODEL_CLASSES[names[mid]]._from_params([float(p) for p in params], Resolution(w, h))
 
         def run(v):
-            L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, v)
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, max(v, -1))
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, 0 if v == -2 else -1)
             return util.sample_points(m, a.cells)
 
-        VS = [int(x) for x in os.environ.get("VARIANTS", "0,1,2,3").split(",")]
+        VS = [int(x) for x in os.environ.get("VARIANTS", "-1,-2,0,2").split(",")]
         res = {v: run(v) for v in VS}
         same = all(torch.equal(res[VS[0]][k], res[v][k]) for k in (0, 1) for v in VS)
         kept = int(res[VS[0]][0].shape[0])
@@ -49,14 +52,16 @@ def main():
                     run(v)
                 e1.record()
                 torch.cuda.synchronize()
-                k = {0: "two_pass", 1: "fused_r2", 2: "fused_r4", 3: "fused_r8"}[v]
+                k = {-1: "segment", -2: "segment_nocert", 0: "two_pass", 1: "fused_r2",
+                     2: "fused_r4", 3: "fused_r8"}[v]
                 cells[k] = min(cells.get(k, 1e9), e0.elapsed_time(e1) / 3)
         L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, -1)
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, -1)
         out[mid] = {"kept": kept, "identical": same,
                     **{k: {"ms": round(v, 4), "Gcells_s": round(a.cells / v / 1e6, 1)}
                        for k, v in cells.items()}}
         print(json.dumps({"model": mid, **out[mid]}), flush=True)
-    print(json.dumps({"what": "sample_points fused vs two-pass", "cells": a.cells,
+    print(json.dumps({"what": "sample_points paths", "cells": a.cells,
                       "models": out}))
 
 
