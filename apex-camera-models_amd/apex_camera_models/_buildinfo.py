@@ -23,3 +23,13 @@ def source_sha256() -> str:
         with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()
+
+
+def lib_identity(lib_path: str) -> dict:
+    """The library file's name and its acm_version() string, which names the
+    compile-time variant (ACM_IEEE_MATH, diagnostic defines): a PMC summary
+    is attributed to a rebuilt library only if both match (bench.py)."""
+    import ctypes
+    L = ctypes.CDLL(lib_path)
+    L.acm_version.restype = ctypes.c_char_p
+    return {"name": os.path.basename(lib_path), "version": L.acm_version().decode()}

@@ -85,6 +85,27 @@ __host__ __device__ inline void unproject_consts(int model, const T* p, T* uk) {
         const T b = T(4) * fabs(p[4]) + T(16) * fabs(p[5]) + T(64) * fabs(p[6]) +
                     T(256) * fabs(p[7]);
         uk[0] = b <= T(63) ? T(1) : T(NAN);
+        // uk[1]: the status of a NaN pixel -- the reference loop
+        // (kannala_brandt.rs:474-511) on ru = min(NaN, pi/2) = pi/2, in its
+        // own operation order (this file is built -ffp-contract=off)
+        {
+            const T k1 = p[4], k2 = p[5], k3 = p[6], k4 = p[7];
+            const T ru = T(kPi / 2.0);
+            T theta = ru;
+            bool conv = true;
+            for (int i = 0; i < 10; ++i) {
+                T t2 = theta * theta, t4 = t2 * t2, t6 = t4 * t2, t8 = t4 * t4;
+                T a = k1 * t2, bb = k2 * t4, cc = k3 * t6, d = k4 * t8;
+                T f = theta * (T(1) + a + bb + cc + d) - ru;
+                T fp = T(1) + (T(3) * a) + (T(5) * bb) + (T(7) * cc) + (T(9) * d);
+                if (fabs(fp) < T(kEps)) { conv = false; break; }
+                T delta = f / fp;
+                theta -= delta;
+                if (fabs(delta) < T(1e-6)) break;
+                if (i == 9) conv = false;
+            }
+            uk[1] = conv ? T(ST_OK) : T(ST_NUMERICAL_ERROR);
+        }
     } else if (model == ACM_RADTAN) {
         // uk[0]: the certified fast Newton of RadTan::unproject (1) or not
         // (NaN); its error bound assumes |rad| <= 16 for |x|, |y| <= 2.
@@ -3636,6 +3657,21 @@ ACM_API int acm_set_tuning(int key, int value) {
 
 ACM_API int acm_last_hip_error(void) { return g_last_hip_error; }
 ACM_API const char* acm_last_error(void) { return g_last_error.c_str(); }
-ACM_API const char* acm_version(void) { return "acm 0.1.0 (gfx950)"; }
+// The version string names the compile-time variant of the build (the
+// diagnostic / A-B defines), so a counter file collected on one variant
+// cannot be attributed to another (bench.py load_traffic).
+ACM_API const char* acm_version(void) {
+    return "acm 0.3.0 (gfx950"
+#ifdef ACM_IEEE_MATH
+           "; ACM_IEEE_MATH"
+#endif
+#ifdef ACM_DIAG_SAMPLE
+           "; ACM_DIAG_SAMPLE"
+#endif
+#ifdef ACM_DIAG_REFILL
+           "; ACM_DIAG_REFILL"
+#endif
+           ")";
+}
 
 }  // extern "C"

@@ -504,6 +504,16 @@ struct RadTan {
             X = Y = Z = T(NAN);
             return s.st;
         }
+        // A NaN pixel passes the bounds test (every comparison is false) and
+        // the reference then iterates on NaN errors until MAX_ITERATIONS:
+        // NumericalError (:514-520), as newton_step's NaN exit returns.
+        // Taken here, before the fast loop, so a failed projection's NaN
+        // pixel (an unfiltered round trip has ~13% of them) does not send
+        // its whole wave through the reference loop's first step.
+        if (!(s.tx == s.tx && s.ty == s.ty)) {
+            X = Y = Z = T(NAN);
+            return ST_NUMERICAL_ERROR;
+        }
 #ifndef ACM_IEEE_MATH
         if constexpr (sizeof(T) == 8) {
             T px, py;  // uk[0] NaN: unbounded terms, or ACM_TUNE_NEWTON_FAST = 0
@@ -711,6 +721,15 @@ struct KannalaBrandt {
         bool certified = false;
 #ifndef ACM_IEEE_MATH
         if constexpr (sizeof(T) == 8) {
+            // A NaN pixel: ru = min(NaN, pi/2) = pi/2 (f64::min returns the
+            // other operand, :467), the loop runs on that constant, and the
+            // ray is NaN (mx / ru); the status of that run is a camera
+            // constant, precomputed on the host by the same reference loop
+            // (uk[1], unproject_consts).  Skips the reference loop per pixel.
+            if (r2 != r2) {
+                X = Y = Z = T(NAN);
+                return (uint8_t)c.uk[1];
+            }
             certified = front_fast(c, r2, ru, theta, ir_fast);
             if (KEEP && certified && fabs(fabs(theta) - T(kHalfPiDown)) <= T(1e-11))
                 certified = false;  // too close to call: take the reference's theta

@@ -188,9 +188,14 @@ def load_traffic(workload, n):
     # hipcc output is not byte-reproducible: accept a rebuild of the very
     # same sources (and build recipe), provided the library is newer than
     # every source file (so it was built from them)
-    from apex_camera_models import _lib
+    # The source hash ignores compile defines and which library file ran, so
+    # the summary must also name this very build variant: the same file name
+    # and acm_version() (which lists the defines) -- a counter file from a
+    # diagnostic build is never reported for the production library.
+    from apex_camera_models import _buildinfo, _lib
     src_ok = d.get("libacm_source_sha256") is not None and \
-        d["libacm_source_sha256"] == _lib.source_sha256()
+        d["libacm_source_sha256"] == _lib.source_sha256() and \
+        d.get("libacm_identity") == _buildinfo.lib_identity(_lib.LIB_PATH)
     if src_ok and os.path.getmtime(_lib.LIB_PATH) >= _latest_source_mtime():
         return d["hbm_bytes_per_launch"], rel + " (same libacm sources, rebuilt library)"
     return None, f"{rel} was collected on another libacm.so build (stale): not reported"

@@ -82,6 +82,7 @@ def main():
                        "WRITE_SIZE KiB x1024",
         "libacm_sha256": hashlib.sha256(open(a.lib, "rb").read()).hexdigest(),
         "libacm_source_sha256": source_sha256(),
+        "libacm_identity": _buildinfo.lib_identity(a.lib),
     }
     if a.algorithmic_bytes and out["hbm_bytes_per_launch"]:
         out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / a.algorithmic_bytes

@@ -45,10 +45,29 @@ def test_same_library_bytes(root):
     assert t == 1.7e9 and src.endswith("x_pmc_test.json")
 
 
+def _ident():
+    from apex_camera_models import _buildinfo
+    return _buildinfo.lib_identity(_lib.LIB_PATH)
+
+
 def test_rebuild_of_same_sources(root):
-    _write(root, libacm_sha256="0" * 64, libacm_source_sha256=_lib.source_sha256())
+    _write(root, libacm_sha256="0" * 64, libacm_source_sha256=_lib.source_sha256(),
+           libacm_identity=_ident())
     t, src = bench.load_traffic(WL, 10_000_000)
     assert t == 1.7e9 and "same libacm sources" in src
+
+
+def test_same_sources_other_build_variant_is_not_reported(root):
+    """a summary collected on a diagnostic / A-B build of the same
+    sources (another file, other -D defines in acm_version) is not this
+    library's traffic; neither is one that does not name its build."""
+    for ident in ({"name": "libacm_diag1.so", "version": _ident()["version"]},
+                  {"name": "libacm.so", "version": "acm 0.3.0 (gfx950; ACM_DIAG_SAMPLE)"},
+                  None):
+        _write(root, libacm_sha256="0" * 64, libacm_source_sha256=_lib.source_sha256(),
+               libacm_identity=ident)
+        t, src = bench.load_traffic(WL, 10_000_000)
+        assert t is None and "stale" in src, ident
 
 
 def test_other_build_is_not_reported(root):
@@ -58,7 +77,8 @@ def test_other_build_is_not_reported(root):
 
 
 def test_sources_newer_than_library_are_not_trusted(root):
-    _write(root, libacm_sha256="0" * 64, libacm_source_sha256=_lib.source_sha256())
+    _write(root, libacm_sha256="0" * 64, libacm_source_sha256=_lib.source_sha256(),
+           libacm_identity=_ident())
     f = root / "apex-camera-models_amd" / "csrc" / "acm.hip"
     future = os.path.getmtime(_lib.LIB_PATH) + 100
     os.utime(f, (future, future))
