@@ -72,6 +72,7 @@ TUNE_SAMPLE_FUSED, TUNE_UNPROJECT_RCP, TUNE_SAMPLE_PATIENCE = 9, 10, 11
 TUNE_NEWTON_FAST = 12  # removed in round 3: acm_set_tuning rejects it (use REFERENCE_NEWTON)
 TUNE_UNPROJECT_PPT = 13
 TUNE_SAMPLE_CERT = 14
+TUNE_SAMPLE_WRITE = 15
 ERR_NOT_SUPPORTED = -6
 ERR_NUMERICAL = -7
 LM_TERMINATION = {0: "MaxIterations", 1: "CostTolerance", 2: "ParameterTolerance",

@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -133,6 +134,7 @@ __host__ __device__ inline void unproject_consts(int model, const T* p, T* uk) {
 struct CamArg : acm_camera {
     double ifx, ify;
     double uk[4];
+    double kc[9];  // KB sample_points: certified kept interval + initial guess (Cam::kc)
 };
 
 template <class T>
@@ -146,6 +148,9 @@ __device__ __forceinline__ Cam<T> make_cam(const acm_camera& c) {
     k.hi = c.height;
     k.ifx = k.ify = T(0);  // divide
     unproject_consts<T>(c.model, k.p, k.uk);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) k.kc[i] = T(0);
+    k.kc[0] = T(INFINITY);  // no certified interval (sample_points only)
     return k;
 }
 
@@ -163,6 +168,8 @@ __device__ __forceinline__ Cam<T> make_cam(const CamArg& c) {
     k.ify = c.ify;
 #pragma unroll
     for (int i = 0; i < 4; ++i) k.uk[i] = c.uk[i];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) k.kc[i] = c.kc[i];
     return k;
 }
 
@@ -1449,14 +1456,17 @@ constexpr size_t kSegBlockCells = (size_t)kSegCells * kSegPerBlock;
 
 enum : int { SEG_UNKNOWN = 0, SEG_ALL = 1, SEG_NONE = 2 };
 
-// Host-certified keep regions, in the model's certificate variable q (KB: ru
-// = min(sqrt(r2), pi/2); the other models: r2).  Every cell whose q lies in
-// [all_lo, all_hi] is kept, every cell in [none_lo, none_hi] is not (both
-// intervals empty when on == 0: every segment is decided cell by cell).
+// Keep certificates.  KB: host-certified regions in ru = min(sqrt(r2), pi/2)
+// (kb_seg_cert): every cell whose ru lies in [all_lo, all_hi] is kept, none
+// in [none_lo, none_hi].  Pinhole, FOV, DS, UCM, EUCM: on = 1 and the
+// segment's r2 interval is pushed through the model's closed form in
+// interval arithmetic on the device (seg_keep_iv).  RadTan, or on = 0
+// (ACM_TUNE_SAMPLE_CERT = 0): every segment is decided cell by cell.
 struct SegCert {
     int on;
-    int in_bounds_checked;  // 1: the model's unprojection has the image-bounds test
+    int ig_ok;  // KB: ig[] fits theta*(ru) on [0, all_hi] well enough for ray_certified
     double all_lo, all_hi, none_lo, none_hi;
+    double ig[7];  // KB: theta*(ru) ~= ru * sum ig[i] ru^(2i)
 };
 
 // Rigorous bounds of r2 = mx^2 + my^2 over the cells [c0, c1] (inclusive,
@@ -1494,21 +1504,161 @@ __device__ __forceinline__ bool seg_r2_bounds(const Cam<double>& c, const Grid& 
     return inb && lo == lo && hi == hi;
 }
 
+// Interval arithmetic for the segment certificates: every operation returns
+// an enclosure of its exact result widened by 2^-40 of the operands'
+// magnitude (plus 2^-1000 absolute).  That covers the operation's own
+// rounding and, by induction, the few-ulp rounding of the same expression
+// evaluated per cell in double: every double the kernels compute for a cell
+// whose r2 lies in the input interval lies inside the result.  A NaN
+// anywhere (sqrt of a possibly negative value, 0 in a divisor) is reported
+// as `nan` and the segment is left to the cells.
+struct Iv {
+    double lo, hi;
+    bool nan;
+};
+__device__ __forceinline__ Iv iv_mk(double lo, double hi, double mag, bool nan) {
+    const double e = mag * 0x1p-40 + 0x1p-1000;
+    return Iv{lo - e, hi + e, nan || !(lo == lo) || !(hi == hi)};
+}
+__device__ __forceinline__ Iv iv_c(double x) { return Iv{x, x, !(x == x)}; }
+__device__ __forceinline__ Iv operator+(Iv a, Iv b) {
+    return iv_mk(a.lo + b.lo, a.hi + b.hi, fmax(fabs(a.lo), fabs(a.hi)) + fmax(fabs(b.lo), fabs(b.hi)),
+                 a.nan || b.nan);
+}
+__device__ __forceinline__ Iv operator-(Iv a, Iv b) {
+    return iv_mk(a.lo - b.hi, a.hi - b.lo, fmax(fabs(a.lo), fabs(a.hi)) + fmax(fabs(b.lo), fabs(b.hi)),
+                 a.nan || b.nan);
+}
+__device__ __forceinline__ Iv operator*(Iv a, Iv b) {
+    const double p0 = a.lo * b.lo, p1 = a.lo * b.hi, p2 = a.hi * b.lo, p3 = a.hi * b.hi;
+    const double lo = fmin(fmin(p0, p1), fmin(p2, p3)), hi = fmax(fmax(p0, p1), fmax(p2, p3));
+    return iv_mk(lo, hi, fmax(fabs(lo), fabs(hi)), a.nan || b.nan);
+}
+__device__ __forceinline__ Iv operator/(Iv a, Iv b) {
+    if (!(b.lo > 0.0 || b.hi < 0.0)) return Iv{-INFINITY, INFINITY, true};
+    const double p0 = a.lo / b.lo, p1 = a.lo / b.hi, p2 = a.hi / b.lo, p3 = a.hi / b.hi;
+    const double lo = fmin(fmin(p0, p1), fmin(p2, p3)), hi = fmax(fmax(p0, p1), fmax(p2, p3));
+    return iv_mk(lo, hi, fmax(fabs(lo), fabs(hi)), a.nan || b.nan);
+}
+__device__ __forceinline__ Iv iv_sqrt(Iv a) {
+    if (!(a.lo >= 0.0)) return Iv{0.0, sqrt(fmax(a.hi, 0.0)) * 2.0 + 1.0, true};
+    const double lo = sqrt(a.lo), hi = sqrt(a.hi);
+    return iv_mk(lo, hi, hi, a.nan);
+}
+__device__ __forceinline__ Iv iv_sq(Iv a) {  // a * a, >= 0
+    const double m = fmax(fabs(a.lo), fabs(a.hi));
+    const double n = (a.lo <= 0.0 && a.hi >= 0.0) ? 0.0 : fmin(fabs(a.lo), fabs(a.hi));
+    return iv_mk(n * n, m * m, m * m, a.nan);
+}
+
+// keep = status Ok && z > 0 && |p| finite, from the r2 interval of a segment.
+// The closed forms follow the unprojections in camera_models.hpp operation
+// by operation (double_sphere.rs:436-476, ucm.rs:337-367, eucm.rs:368-398).
+__device__ __forceinline__ int seg_from(bool fail_all, bool fail_none, Iv z, Iv n2) {
+    if (fail_all || (!z.nan && z.hi < 0.0)) return SEG_NONE;
+    if (fail_none && !z.nan && !n2.nan && z.lo > 0.0 && n2.hi < 1e300) return SEG_ALL;
+    return SEG_UNKNOWN;
+}
+
+template <class TagT>
+__device__ __forceinline__ int seg_keep_iv(const Cam<double>& c, const SegCert& k, double r2lo,
+                                           double r2hi) {
+    return SEG_UNKNOWN;  // RadTan: Newton in (x, y), not a function of r2 alone
+}
+template <>
+__device__ __forceinline__ int seg_keep_iv<Tag<KannalaBrandt>>(const Cam<double>& c,
+                                                               const SegCert& k, double lo,
+                                                               double hi) {
+    // the host certificate, in ru = min(sqrt(r2), pi/2) (:462-467)
+    constexpr double kHalfPi = kPi / 2.0;
+    const double qlo = fmin(sqrt(lo) * (1.0 - 0x1p-40), kHalfPi);
+    const double qhi = fmin(sqrt(hi) * (1.0 + 0x1p-40), kHalfPi);
+    if (qlo >= k.all_lo && qhi <= k.all_hi) return SEG_ALL;
+    if (qlo >= k.none_lo && qhi <= k.none_hi) return SEG_NONE;
+    return SEG_UNKNOWN;
+}
+template <>
+__device__ __forceinline__ int seg_keep_iv<Tag<Pinhole>>(const Cam<double>& c, const SegCert& k,
+                                                         double lo, double hi) {
+    // pinhole.rs:228-246: in the image (checked by the caller) and Z =
+    // 1 / sqrt(1 + r2) > 0, i.e. 1 + r2 finite
+    return hi < 1e300 ? SEG_ALL : SEG_UNKNOWN;
+}
+template <>
+__device__ __forceinline__ int seg_keep_iv<Tag<Fov>>(const Cam<double>& c, const SegCert& k,
+                                                     double lo, double hi) {
+    // fov.rs:336-363: always Ok, z = 1 / |p| > 0 while |p| is finite, and
+    // p = (m * sin(rd w) / (rd 2 tan(w/2))) / cos(rd w) stays finite while
+    // rd w <= 0.99 pi/2 (cos(rd w) >= 0.0157) and r2 is moderate
+    const double wf = c.p[4];
+    if (!(wf > 0.0 && wf < INFINITY) || !(c.p[8] > 0.0)) return SEG_UNKNOWN;
+    const double lim = 0.99 * (kPi / 2.0) / wf;
+    return hi < lim * lim * (1.0 - 0x1p-30) && hi < 1e100 ? SEG_ALL : SEG_UNKNOWN;
+}
+template <>
+__device__ __forceinline__ int seg_keep_iv<Tag<DoubleSphere>>(const Cam<double>& c,
+                                                              const SegCert& k, double lo,
+                                                              double hi) {
+    const double alpha = c.p[4], xi = c.p[5];
+    const Iv r2{lo, hi, false};
+    // reject = alpha != 0 && alpha > 0.5 && r2 > 1 / (2 alpha - 1) (uk[0])
+    const bool rej_on = alpha != 0.0 && alpha > 0.5;
+    const bool rej_all = rej_on && lo > c.uk[0], rej_none = !rej_on || hi <= c.uk[0];
+    const Iv a = iv_c(alpha), one = iv_c(1.0);
+    const Iv mz = (one - a * a * r2) / (a * iv_sqrt(one - (iv_c(2.0) * a - one) * r2) +
+                                        iv_c(1.0 - alpha));
+    const Iv mz2 = iv_sq(mz);
+    const Iv num = mz * iv_c(xi) + iv_sqrt(mz2 + (one - iv_c(xi) * iv_c(xi)) * r2);
+    const Iv den = mz2 + r2;
+    const Iv coeff = num / den;
+    const Iv pz = coeff * mz - iv_c(xi);
+    const Iv n2 = iv_sq(coeff) * r2 + iv_sq(pz);
+    const bool den_fail_all = !den.nan && den.hi < 1e-3, den_fail_none = !den.nan && den.lo >= 1e-3;
+    return seg_from(rej_all || den_fail_all, rej_none && den_fail_none, pz, n2);
+}
+template <>
+__device__ __forceinline__ int seg_keep_iv<Tag<Ucm>>(const Cam<double>& c, const SegCert& k,
+                                                     double lo, double hi) {
+    const double alpha = c.p[4], xi = c.uk[0], gamma = 1.0 - alpha;
+    // mx, my are scaled by gamma (ucm.rs:346-347): r2 = gamma^2 (mx0^2 + my0^2)
+    const Iv r2 = iv_c(gamma * gamma) * Iv{lo, hi, false};
+    const Iv one = iv_c(1.0);
+    const Iv num = iv_c(xi) + iv_sqrt(one + (one - iv_c(xi) * iv_c(xi)) * r2);
+    const Iv den = one - r2;  // the reference's 1 - r^2 (:354)
+    const bool cond_on = alpha > 0.5;
+    const bool cond_all_fail = cond_on && !r2.nan && r2.lo > c.uk[1] * (1.0 + 0x1p-30);
+    const bool cond_none_fail = !cond_on || (!r2.nan && r2.hi <= c.uk[1] * (1.0 - 0x1p-30));
+    const Iv coeff = num / den;
+    const Iv pz = coeff - iv_c(xi);
+    const Iv n2 = iv_sq(coeff) * r2 + iv_sq(pz);
+    const bool den_fail_all = !den.nan && den.hi < 1e-3, den_fail_none = !den.nan && den.lo >= 1e-3;
+    return seg_from(cond_all_fail || den_fail_all, cond_none_fail && den_fail_none, pz, n2);
+}
+template <>
+__device__ __forceinline__ int seg_keep_iv<Tag<Eucm>>(const Cam<double>& c, const SegCert& k,
+                                                      double lo, double hi) {
+    const double alpha = c.p[4], beta = c.p[5];
+    const Iv r2{lo, hi, false};
+    const Iv one = iv_c(1.0), a = iv_c(alpha), b = iv_c(beta);
+    const Iv num = one - r2 * a * a * b;
+    const Iv det = one - (a - iv_c(1.0 - alpha)) * b * r2;
+    const Iv den = iv_c(1.0 - alpha) + a * iv_sqrt(det);
+    // cond = !(alpha > 0.5 && r2 > uk[0]) (eucm.rs:196, precedence quirk kept)
+    const bool cond_on = alpha > 0.5;
+    const bool cond_all_fail = cond_on && lo > c.uk[0], cond_none_fail = !cond_on || hi <= c.uk[0];
+    const Iv mz = num / den;
+    const Iv n2 = r2 + iv_sq(mz);
+    const bool det_fail_all = !det.nan && det.hi < 1e-3, det_fail_none = !det.nan && det.lo >= 1e-3;
+    return seg_from(cond_all_fail || det_fail_all, cond_none_fail && det_fail_none, mz, n2);
+}
+
 template <class TagT>
 __device__ __forceinline__ int seg_classify(const Cam<double>& c, const Grid& g, const SegCert& k,
                                             uint64_t c0, uint64_t c1) {
     if (!k.on) return SEG_UNKNOWN;
     double lo, hi;
     if (!seg_r2_bounds(c, g, c0, c1, lo, hi)) return SEG_UNKNOWN;
-    double qlo = lo, qhi = hi;
-    if constexpr (std::is_same<TagT, Tag<KannalaBrandt>>::value) {
-        constexpr double kHalfPi = kPi / 2.0;  // the reference's clamp, :467
-        qlo = fmin(sqrt(lo) * (1.0 - 0x1p-40), kHalfPi);
-        qhi = fmin(sqrt(hi) * (1.0 + 0x1p-40), kHalfPi);
-    }
-    if (qlo >= k.all_lo && qhi <= k.all_hi) return SEG_ALL;
-    if (qlo >= k.none_lo && qhi <= k.none_hi) return SEG_NONE;
-    return SEG_UNKNOWN;
+    return seg_keep_iv<TagT>(c, k, lo, hi);
 }
 
 template <class TagT>
@@ -1554,45 +1704,66 @@ __global__ __launch_bounds__(kBlock) void k_seg_count(CamArg cam, Grid g, size_t
     }
 }
 
-template <class TagT>
+// Write pass.  Workgroup b covers kSegBlockW = 4 * SPW segments; its 256
+// lanes first turn the counts of the whole count block the segments sit in
+// (256 segments, 1 KiB) into exclusive offsets in LDS (wave scan + the 4
+// wave totals + the scanned block offset), then each wave writes SPW of the
+// segments -- interleaved (ILV: wave w takes segments w, w + 4, ..., so the
+// four waves of a workgroup write adjacent runs at the same time) or
+// contiguous.  Per segment: the 64 cells are unprojected, the kept lanes
+// ballot their rank, each writes its 16-B pixel at offset + rank, and the
+// compacted rays (3 * kept doubles, staged in the wave's 1.5 KiB of LDS) go
+// out as 16-B pieces.  A segment whose count is 0 is skipped.
+template <class TagT, int SPW, bool ILV>
 __global__ __launch_bounds__(kBlock) void k_seg_write(CamArg cam, Grid g, size_t cells,
                                                       const uint32_t* __restrict__ seg_cnt,
                                                       const uint64_t* __restrict__ blk_off,
                                                       double* __restrict__ uv_out,
                                                       double* __restrict__ xyz_out) {
+    static_assert(kSegPerBlock % (4 * SPW) == 0, "write workgroups tile the count blocks");
     const Cam<double> c = make_cam<double>(cam);
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nseg = (cells + kSegCells - 1) / kSegCells;
-    const uint64_t seg = (uint64_t)blockIdx.x * kSegPerBlock + threadIdx.x;
-    // offsets of this workgroup's 256 segments: block offset + exclusive scan
-    const uint32_t cnt = seg < nseg ? seg_cnt[seg] : 0u;
-    uint32_t x = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
+    const uint64_t wseg0 = (uint64_t)blockIdx.x * (4 * SPW);    // this workgroup's first segment
+    const uint64_t cb = wseg0 / kSegPerBlock;                     // its count block
+    __shared__ uint64_t s_off[kSegPerBlock];
+    __shared__ uint32_t s_cnt[kSegPerBlock];
     __shared__ uint32_t s_wsum[kBlock / 64];
     __shared__ double s_ray[kBlock / 64][64 * 3];
-    if (lane == 63) s_wsum[wid] = x;
-    __syncthreads();
-    uint64_t base_off = blk_off[blockIdx.x];
-    for (int w = 0; w < wid; ++w) base_off += s_wsum[w];
-    const uint64_t my_off = base_off + (x - cnt);  // lane l: offset of segment wseg0 + l
+    {
+        const uint64_t sg = cb * kSegPerBlock + threadIdx.x;
+        const uint32_t cnt = sg < nseg ? seg_cnt[sg] : 0u;
+        uint32_t x = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) s_wsum[wid] = x;
+        __syncthreads();
+        uint64_t o = blk_off[cb];
+        for (int w = 0; w < wid; ++w) o += s_wsum[w];
+        s_off[threadIdx.x] = o + (x - cnt);
+        s_cnt[threadIdx.x] = cnt;
+        __syncthreads();
+    }
     const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
     double* lx = s_ray[wid];
-    const uint64_t wseg0 = seg - lane;
+    // the wave's cells, walked incrementally (one scalar division per wave:
+    // a 64-bit division per segment cost more SALU time than Pinhole's math)
+    constexpr uint32_t kStep = ILV ? 4 * kSegCells : kSegCells;
+    const int li0 = (int)(wseg0 - cb * kSegPerBlock) + (ILV ? wid : SPW * wid);
     CellWalk cw;
-    cw.init(g, wseg0 * kSegCells, lane);
+    cw.init(g, (cb * kSegPerBlock + (uint64_t)li0) * kSegCells, lane);
 #pragma unroll 1
-    for (int k = 0; k < 64; ++k, cw.template step_by<kSegCells>(g)) {
-        const uint64_t sg = wseg0 + (uint64_t)k;
+    for (int k = 0; k < SPW; ++k, cw.template step_by<kStep>(g)) {
+        const int li = li0 + (ILV ? 4 * k : k);
+        const uint64_t sg = cb * kSegPerBlock + (uint64_t)li;
         if (sg >= nseg) break;
-        const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)cnt, k);
+        const uint32_t sc = __builtin_amdgcn_readfirstlane(s_cnt[li]);
         if (sc == 0) continue;  // nothing kept here (certified or counted)
-        const uint64_t off = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_off >> 32), k) << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_off, k);
+        const uint64_t off = uniform64(s_off[li]);
         const uint64_t cell = sg * kSegCells + lane;
         double u = 0.0, v = 0.0, X = 0.0, Y = 0.0, Z = 0.0;
         bool keep = false;
@@ -2594,6 +2765,8 @@ static CamArg prep(acm_camera c, bool reference_newton = false) {
     if (reference_newton &&
         (c.model == ACM_KANNALA_BRANDT || c.model == ACM_RADTAN || c.model == ACM_FOV))
         a.uk[0] = NAN;  // fast Newton loops / FOV fast unprojection off
+    for (int i = 0; i < 9; ++i) a.kc[i] = 0.0;
+    a.kc[0] = INFINITY;  // no certified interval (set by acm_sample_points_ex for KB)
     return a;
 }
 
@@ -2675,6 +2848,7 @@ static SegCert kb_seg_cert_on(const double* p, double tmax) {
     const double m = ef + 1e-9;
     constexpr double kHpd = KannalaBrandt<double>::kHalfPiDown;
     s.on = 1;
+    s.ig[0] = M;  // passed to kb_fit_initial_guess (overwritten by the fit)
     s.all_lo = 1e-6 * (1.0 + 1e-6);
     s.all_hi = R;
     if (kHpd - m <= tmax && thd(kHpd - m) < R)  // theta* reaches pi/2 below R
@@ -2693,6 +2867,62 @@ static SegCert kb_seg_cert_on(const double* p, double tmax) {
 // then counted cell by cell.  The theta range the bounds cover is tried at a
 // few sizes (a strongly distorted camera's f' may vanish near theta = 2 but
 // not below pi/2); the certificate covering the most is kept.
+// KB: theta*(ru) ~= ru g(ru^2), g the degree-6 interpolant of theta*(ru)/ru
+// in s = ru^2 at Chebyshev nodes on [0, all_hi^2] (theta* solved in long
+// double).  Accepted for ray_certified only if, over 4001 points of the
+// interval, the error e0 keeps two Newton steps exact to ~1e-13
+// (M^3 e0^4 <= 1e-13, M as in kb_seg_cert_on) and below 1e-5.
+static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
+    s.ig_ok = 0;
+    const long double k1 = p[4], k2 = p[5], k3 = p[6], k4 = p[7];
+    auto root = [&](long double ru) {
+        long double t = ru;
+        for (int i = 0; i < 80; ++i) {
+            const long double t2 = t * t;
+            const long double f = t * (1 + t2 * (k1 + t2 * (k2 + t2 * (k3 + t2 * k4)))) - ru;
+            const long double fp = 1 + t2 * (3 * k1 + t2 * (5 * k2 + t2 * (7 * k3 + t2 * 9 * k4)));
+            const long double d = f / fp;
+            t -= d;
+            if (std::fabs((double)d) < 1e-19) break;
+        }
+        return t;
+    };
+    const double R = s.all_hi;
+    if (!(R > 1e-3)) return;
+    constexpr int N = 7;
+    long double A[N][N + 1];
+    const long double S = (long double)R * R;
+    for (int j = 0; j < N; ++j) {
+        const long double sj = S * (1 + std::cos(kPi * (j + 0.5) / N)) / 2;
+        const long double ru = std::sqrt(sj);
+        const long double gj = ru > 0 ? root(ru) / ru : 1;
+        long double pw = 1;
+        for (int i = 0; i < N; ++i, pw *= sj) A[j][i] = pw;
+        A[j][N] = gj;
+    }
+    for (int c = 0; c < N; ++c) {  // Gauss-Jordan with partial pivoting
+        int piv = c;
+        for (int r = c + 1; r < N; ++r)
+            if (std::fabs((double)A[r][c]) > std::fabs((double)A[piv][c])) piv = r;
+        for (int k = 0; k <= N; ++k) std::swap(A[c][k], A[piv][k]);
+        if (A[c][c] == 0) return;
+        for (int r = 0; r < N; ++r) {
+            if (r == c) continue;
+            const long double f = A[r][c] / A[c][c];
+            for (int k = c; k <= N; ++k) A[r][k] -= f * A[c][k];
+        }
+    }
+    for (int i = 0; i < N; ++i) s.ig[i] = (double)(A[i][N] / A[i][i]);
+    double e0 = 0.0;
+    for (int i = 0; i <= 4000; ++i) {
+        const double ru = R * i / 4000.0;
+        double g = s.ig[N - 1];
+        for (int k = N - 2; k >= 0; --k) g = std::fma(g, ru * ru, s.ig[k]);
+        e0 = std::fmax(e0, std::fabs((double)((long double)ru * g - root(ru))));
+    }
+    s.ig_ok = e0 <= 1e-5 && M * M * M * e0 * e0 * e0 * e0 <= 1e-13;
+}
+
 static SegCert kb_seg_cert(const double* p) {
     SegCert best{};
     best.all_lo = best.none_lo = INFINITY;
@@ -2709,18 +2939,42 @@ static SegCert kb_seg_cert(const double* p) {
             best = s;
         }
     }
+    if (best.on && best.all_hi > best.all_lo) kb_fit_initial_guess(p, best.ig[0], best);
     return best;
+}
+
+// kb_seg_cert costs ~1 ms of host time: memoised per distortion vector
+// (thread-safe; a handful of cameras in practice)
+static SegCert kb_seg_cert_cached(const double* p) {
+    static std::mutex mu;
+    static std::map<std::array<double, 4>, SegCert> memo;
+    const std::array<double, 4> key{p[4], p[5], p[6], p[7]};
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = memo.find(key);
+        if (it != memo.end()) return it->second;
+    }
+    const SegCert c = kb_seg_cert(p);
+    std::lock_guard<std::mutex> lock(mu);
+    if (memo.size() > 256) memo.clear();
+    memo[key] = c;
+    return c;
 }
 
 // ACM_TUNE_SAMPLE_CERT: -1 auto = on, 0 = off (every segment counted cell by cell)
 static std::atomic<int> g_sample_cert{-1};
+// ACM_TUNE_SAMPLE_WRITE: the segment write pass's layout (see its launch)
+static std::atomic<int> g_sample_write{-1};
 
 static SegCert seg_cert(const acm_camera& cam) {
     SegCert s{};
     s.all_lo = s.none_lo = INFINITY;
     s.all_hi = s.none_hi = -INFINITY;
     if (g_sample_cert == 0) return s;
-    if (cam.model == ACM_KANNALA_BRANDT) return kb_seg_cert(cam.params);
+    if (cam.model == ACM_KANNALA_BRANDT) return kb_seg_cert_cached(cam.params);
+    // the closed-form models (and Pinhole, FOV) are certified per segment on
+    // the device (seg_keep_iv); RadTan's Newton runs in (x, y): no certificate
+    if (cam.model != ACM_RADTAN) s.on = 1;
     return s;
 }
 
@@ -3271,7 +3525,17 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
     const int pat = g_sample_patience;
     g.patience = pat < 0 ? kLbPatience : pat;
     hipStream_t s = (hipStream_t)stream;
-    const CamArg ca = prep(*cam, refn);
+    CamArg ca = prep(*cam, refn);
+    if (cam->model == ACM_KANNALA_BRANDT && !refn) {
+        // the certified kept interval + initial guess for ray_certified, in
+        // every sample_points path alike (same rays whichever kernels run)
+        const SegCert kc = kb_seg_cert_cached(cam->params);
+        if (kc.on && kc.ig_ok && kc.all_hi > kc.all_lo) {
+            ca.kc[0] = kc.all_lo;
+            ca.kc[1] = kc.all_hi;
+            for (int i = 0; i < 7; ++i) ca.kc[2 + i] = kc.ig[i];
+        }
+    }
     if (!cells) {  // nothing to launch: counts = [0 kept, 0 cells]
         if (hipMemsetAsync(counts, 0, 2 * sizeof(uint64_t), s) != hipSuccess)
             return check_launch("acm_sample_points: counts");
@@ -3279,7 +3543,12 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
     }
     // (plain stores: non-temporal ones measured slower for these compacted
     // outputs, 1.41 -> 1.47 ms at 1e8 KB cells, profiles/r02_diag_sample_phases.log)
-    const int mode = g_sample_fused;
+    int mode = g_sample_fused;
+    // RadTan has no keep certificate (its Newton runs in (x, y), not on r2):
+    // the segment path would count every cell with the full Newton, so auto
+    // keeps the single pass for it (1.32 vs 1.78 ms at 1e8 cells,
+    // profiles/r03c_diag_sample.log)
+    if (mode < 0 && cam->model == ACM_RADTAN) mode = 2;
     if (mode < 0) {  // segment two-pass (default)
         const size_t nseg = (cells + kSegCells - 1) / kSegCells;
         const size_t nsb = (cells + kSegBlockCells - 1) / kSegBlockCells;
@@ -3293,8 +3562,20 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
                                cells, cert, seg_cnt, blk_sum);
             hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, blk_sum, nsb, blk_off,
                                counts, (uint64_t)cells);
-            hipLaunchKernelGGL((k_seg_write<TagT>), dim3((unsigned)nsb), dim3(kBlock), 0, s, ca, g,
-                               cells, seg_cnt, blk_off, points_2d_out, points_3d_out);
+            // ACM_TUNE_SAMPLE_WRITE: segments per write wave and order
+            // (-1 auto = 16 interleaved; 1 = 64 contiguous, 2 = 16
+            // interleaved, 3 = 4 interleaved, 4 = 16 contiguous)
+            const int wv0 = g_sample_write.load(std::memory_order_relaxed);
+            const int wv = wv0 < 0 ? 2 : wv0;
+            auto wlaunch = [&](auto kern, int spw) {
+                const size_t nwb = (nseg + 4 * (size_t)spw - 1) / (4 * (size_t)spw);
+                hipLaunchKernelGGL(kern, dim3((unsigned)nwb), dim3(kBlock), 0, s, ca, g, cells,
+                                   seg_cnt, blk_off, points_2d_out, points_3d_out);
+            };
+            if (wv == 1) wlaunch(k_seg_write<TagT, 64, false>, 64);
+            else if (wv == 3) wlaunch(k_seg_write<TagT, 4, true>, 4);
+            else if (wv == 4) wlaunch(k_seg_write<TagT, 16, false>, 16);
+            else wlaunch(k_seg_write<TagT, 16, true>, 16);
             return check_launch("acm_sample_points");
         });
     }
@@ -3637,6 +3918,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_UNPROJECT_RCP, &g_unproject_rcp, -1, 1, "value must be -1..1"},
         {ACM_TUNE_SAMPLE_PATIENCE, &g_sample_patience, -1, 1 << 20, "value must be -1..2^20"},
         {ACM_TUNE_SAMPLE_CERT, &g_sample_cert, -1, 0, "value must be -1 (auto) or 0"},
+        {ACM_TUNE_SAMPLE_WRITE, &g_sample_write, -1, 4, "value must be -1..4"},
         {ACM_TUNE_UNPROJECT_PPT, &g_unproject_ppt, -1, 3, "value must be -1..3"},
     };
     if (key == ACM_TUNE_NEWTON_FAST)  // removed (r03): numerics are chosen per call

@@ -263,6 +263,10 @@ struct Cam {
     // point (IEEE results, identical wherever they are computed).
     T ifx, ify;
     T uk[4];
+    // KB sample_points (kc[1] > 0 only there): cells whose ru lies in the
+    // host-certified kept interval [kc[0], kc[1]] (acm.hip kb_seg_cert) take
+    // KannalaBrandt::ray_certified; kc[2..8] = the initial-guess polynomial.
+    T kc[9];
 };
 
 // (u - cx) / fx with fx uniform: RN(a / b) from the host's RN(1 / b) and the
@@ -682,6 +686,49 @@ struct KannalaBrandt {
         ir = clamp ? T(2.0 / kPi) : y;
         return newton_fast(c, ru, theta);
     }
+    // The ray of a cell the host has certified Ok and kept (sample_points):
+    // the status and the keep decision are known, and the ray is held to
+    // 1e-10, so theta need not follow the reference's iterates -- only be
+    // accurate.  The reference stops at |delta| < 1e-6, i.e. within ~M 1e-12
+    // of the root theta* (kb_seg_cert's bound); here theta_0 = ru P(ru^2),
+    // the host's fit of theta*(ru) (error <= 1e-5, checked on the host), then
+    // two Newton steps (error <= M^3 1e-20): theta* to rounding.  1 / ru
+    // from rsq; ru < pi/2 (the certified interval ends below the clamp).
+    __device__ static __forceinline__ void ray_certified(const Cam<T>& c, T mx, T my, T r2, T& X,
+                                                         T& Y, T& Z) {
+        const T k1 = c.p[4], k2 = c.p[5], k3 = c.p[6], k4 = c.p[7];
+        const T ir = rsq_nr(r2);
+        const T ru = r2 * ir;
+        const T s0 = ru * ru;
+        T g = c.kc[8];
+#pragma unroll
+        for (int i = 7; i >= 2; --i) g = fma(g, s0, c.kc[i]);
+        T t = ru * g;
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            const T s = t * t;
+            const T b3 = fma(k4, s, k3);
+            const T c2 = fma(k4, s, b3);
+            const T b2 = fma(b3, s, k2);
+            const T c1 = fma(c2, s, b2);
+            const T b1 = fma(b2, s, k1);
+            const T c0 = fma(c1, s, b1);
+            const T pp = fma(b1, s, T(1));
+            const T fp = fma(s + s, c0, pp);
+            const T f = fma(t, pp, -ru);
+            const T y0 = __builtin_amdgcn_rcp(fp);
+            t -= f * fma(y0, fma(-fp, y0, T(1)), y0);
+        }
+        T sn, cs;
+        sincos_0_2(t, &sn, &cs);
+        const T q = sn * ir;  // sin(theta) / ru
+        const T px = mx * q, py = my * q;
+        const T in = rsq_nr(fma(px, px, fma(py, py, cs * cs)));
+        X = px * in;
+        Y = py * in;
+        Z = cs * in;
+    }
+
     // kannala_brandt.rs:445-562: Newton on theta_d(theta) = ru, <=10 steps.
     __device__ static __forceinline__ uint8_t unproject(const Cam<T>& c, T u, T v, T& X, T& Y,
                                                         T& Z) {
@@ -720,6 +767,17 @@ struct KannalaBrandt {
         bool converged = true;
         bool certified = false;
 #ifndef ACM_IEEE_MATH
+        if constexpr (sizeof(T) == 8 && KEEP) {
+            // sample_points: a cell inside the host-certified kept interval
+            // is Ok and kept whatever its Newton run does (kb_seg_cert), so
+            // only its ray is needed, to 1e-10: ray_certified
+            if (r2 >= c.kc[0] * c.kc[0] * T(1 + 0x1p-30) &&
+                r2 <= c.kc[1] * c.kc[1] * T(1 - 0x1p-30)) {
+                ray_certified(c, mx, my, r2, X, Y, Z);
+                keep = true;
+                return ST_OK;
+            }
+        }
         if constexpr (sizeof(T) == 8) {
             // A NaN pixel: ru = min(NaN, pi/2) = pi/2 (f64::min returns the
             // other operand, :467), the loop runs on that constant, and the

@@ -451,6 +451,10 @@ ACM_API int acm_stream_synchronize(void *stream);
  * Outputs are identical for every value.
  * ACM_TUNE_SAMPLE_CERT: the segment path's host-certified keep regions
  * (-1 = auto = on; 0 = every segment counted cell by cell).  Same outputs.
+ * ACM_TUNE_SAMPLE_WRITE: the segment path's write pass, segments per wave
+ * and their order (-1 = auto = 16 interleaved across the workgroup's four
+ * waves; 1 = 64 contiguous, 2 = 16 interleaved, 3 = 4 interleaved, 4 = 16
+ * contiguous).  Same outputs.
  * ACM_TUNE_UNPROJECT_RCP: unprojections (acm_unproject, acm_sample_points*)
  * divide by fx, fy through the host's correctly rounded 1/fx, 1/fy and one
  * FMA correction, bit-identical to the division (-1 = auto = on, 0 = plain
@@ -485,7 +489,8 @@ enum {
     ACM_TUNE_SAMPLE_PATIENCE = 11,
     ACM_TUNE_NEWTON_FAST = 12,
     ACM_TUNE_UNPROJECT_PPT = 13,
-    ACM_TUNE_SAMPLE_CERT = 14
+    ACM_TUNE_SAMPLE_CERT = 14,
+    ACM_TUNE_SAMPLE_WRITE = 15
 };
 ACM_API int acm_set_tuning(int key, int value);
 

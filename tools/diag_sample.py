@@ -1,7 +1,8 @@
 """sample_points A/B of every path (ACM_TUNE_SAMPLE_FUSED): the segment
-two-pass default (-1; -2 = the same with ACM_TUNE_SAMPLE_CERT = 0, every
-segment counted cell by cell), the round-1 two-pass count / scan / write
-path (0) and the single pass with a decoupled look-back (1 / 2 / 3), every
+two-pass default ("seg"; "seg_nocert" = ACM_TUNE_SAMPLE_CERT 0, every
+segment counted cell by cell; "seg_w1".."seg_w4" = ACM_TUNE_SAMPLE_WRITE),
+the round-1 two-pass count / scan / write path ("two_pass") and the single
+pass with a decoupled look-back ("fused_r2" / "_r4" / "_r8"), every
 model on the config-5 grid (1e8 requested cells), interleaved in one
 process.  The outputs must be bit-identical.
 
@@ -31,12 +32,16 @@ def main():
         params, (w, h) = samples.SAMPLES[mid]
         m = MODEL_CLASSES[names[mid]]._from_params([float(p) for p in params], Resolution(w, h))
 
+        # variant names: seg (default), seg_nocert, seg_w1..seg_w4
+        # (ACM_TUNE_SAMPLE_WRITE), two_pass, fused_r2 / r4 / r8
         def run(v):
-            L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, max(v, -1))
-            L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, 0 if v == -2 else -1)
+            fused = {"two_pass": 0, "fused_r2": 1, "fused_r4": 2, "fused_r8": 3}.get(v, -1)
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, fused)
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, 0 if v == "seg_nocert" else -1)
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_WRITE, int(v[-1]) if v.startswith("seg_w") else -1)
             return util.sample_points(m, a.cells)
 
-        VS = [int(x) for x in os.environ.get("VARIANTS", "-1,-2,0,2").split(",")]
+        VS = os.environ.get("VARIANTS", "seg,seg_nocert,two_pass,fused_r4").split(",")
         res = {v: run(v) for v in VS}
         same = all(torch.equal(res[VS[0]][k], res[v][k]) for k in (0, 1) for v in VS)
         kept = int(res[VS[0]][0].shape[0])
@@ -52,11 +57,10 @@ def main():
                     run(v)
                 e1.record()
                 torch.cuda.synchronize()
-                k = {-1: "segment", -2: "segment_nocert", 0: "two_pass", 1: "fused_r2",
-                     2: "fused_r4", 3: "fused_r8"}[v]
-                cells[k] = min(cells.get(k, 1e9), e0.elapsed_time(e1) / 3)
+                cells[v] = min(cells.get(v, 1e9), e0.elapsed_time(e1) / 3)
         L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, -1)
         L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, -1)
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_WRITE, -1)
         out[mid] = {"kept": kept, "identical": same,
                     **{k: {"ms": round(v, 4), "Gcells_s": round(a.cells / v / 1e6, 1)}
                        for k, v in cells.items()}}
