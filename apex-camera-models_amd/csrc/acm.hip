@@ -600,67 +600,6 @@ template <class TagT> struct UnprojectStaged { static constexpr bool on = true; 
 template <> struct UnprojectStaged<Tag<KannalaBrandt>> { static constexpr bool on = false; };
 template <> struct UnprojectStaged<Tag<RadTan>> { static constexpr bool on = false; };
 
-#ifdef ACM_DIAG_REFILL
-// Diagnostic build (ACM_DIAG_REFILL = K): RadTan acm_unproject with lane
-// refill.  Each wave owns a contiguous chunk of pixels; a lane whose Newton
-// loop has ended writes its ray and status and, once at least K lanes of
-// the wave are idle, the idle lanes take the next pixels of the chunk (in
-// lane order, so the refill loads are contiguous).  Per-point iterates are
-// RadTan::newton_step's, so outputs are bit-identical to k_unproject.
-template <int K>
-__global__ __launch_bounds__(kBlock) void k_unproject_refill(CamArg cam, size_t n,
-                                                             size_t chunk,
-                                                             const double* __restrict__ uv,
-                                                             double* __restrict__ rays,
-                                                             uint8_t* __restrict__ status) {
-    using M = RadTan<double>;
-    const Cam<double> c = make_cam<double>(cam);
-    const int lane = threadIdx.x & 63;
-    const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
-    const size_t wave = (size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    const size_t begin = wave * chunk;
-    const size_t end = begin + chunk < n ? begin + chunk : n;
-    size_t head = begin;
-    size_t idx = 0;
-    bool active = false;
-    M::Newton st;
-    for (;;) {
-        const uint64_t idle = __ballot(!active);
-        if (head < end && (size_t)__popcll(idle) >= (size_t)K) {
-            const size_t cand = head + (size_t)__popcll(idle & below);
-            head += (size_t)__popcll(idle);
-            if (!active && cand < end) {
-                idx = cand;
-                const double2 q = *reinterpret_cast<const double2*>(uv + 2 * idx);
-                if (M::newton_init(c, q.x, q.y, st)) {
-                    active = true;
-                } else {  // outside the image: NaN ray at once
-                    const double nn = __builtin_nan("");
-                    rays[3 * idx] = nn;
-                    rays[3 * idx + 1] = nn;
-                    rays[3 * idx + 2] = nn;
-                    status[idx] = st.st;
-                }
-            }
-            continue;  // re-count: a lane that got an out-of-image pixel is idle again
-        }
-        if (!__ballot(active)) {
-            if (head >= end) break;
-            continue;
-        }
-        if (active && M::newton_step(c, st)) {
-            double X, Y, Z;
-            const uint8_t r = M::newton_finish(st, X, Y, Z);
-            if (r != ST_OK) X = Y = Z = __builtin_nan("");
-            rays[3 * idx] = X;
-            rays[3 * idx + 1] = Y;
-            rays[3 * idx + 2] = Z;
-            status[idx] = r;
-            active = false;
-        }
-    }
-}
-#endif
 
 // -------------------------------------------------- residual + Jacobian
 template <class TagT, int LAYOUT, bool WJ, bool NT>
@@ -832,9 +771,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     constexpr int D = L::D;
     constexpr int K = L::K;
     const Cam<double> c = make_cam<double>(cam);
-    double acc[K];
+    // KB: 37 running sums in its own layout (kKbNe below) instead of K = 40
+    // -- and no 2 x 8 Jacobian held per point -- expanded to NE<8> once per
+    // lane at the end
+    constexpr bool kKB = std::is_same<TagT, Tag<KannalaBrandt>>::value;
+    constexpr int KA = kKB ? 37 : K;
+    double acc[KA];
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    for (int k = 0; k < KA; ++k) acc[k] = 0.0;
     const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
     const size_t stride = (size_t)gridDim.x * kBlock;
     size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -847,6 +791,49 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // multiply-adds: the sums are held to 1e-10, not to the reference's
     // operation order, and the validity mask stays exact (camera_models.hpp).
     auto accumulate = [&](double px, double py, double pz, double2 po) {
+        if constexpr (kKB) {
+            // KB sums (37): [0] a^2 [1] a [2] b^2 [3] b, [4+k] a fxr T_k,
+            // [8+k] b fyr T_k, [12+k] fxr T_k, [16+k] fyr T_k (T_k =
+            // theta^(2k+3), k < 4), [20+m] (fxr^2 + fyr^2) theta^(6+2m)
+            // (m < 7: every du_j du_k + dv_j dv_k with j + k = m), [27] a r0
+            // [28] b r1 [29] r0 [30] r1, [31+k] (fxr r0 + fyr r1) T_k,
+            // [35] r.r (or the sentinel), [36] n_valid
+            double u, v, a, b, fxr, fyr, t2, t3;
+            const uint8_t st = M::project_ne(c, px, py, pz, u, v, a, b, fxr, fyr, t2, t3);
+            if (st == ST_OK) {
+                const double r0 = u - po.x, r1 = v - po.y;
+                acc[0] = fma(a, a, acc[0]);
+                acc[1] += a;
+                acc[2] = fma(b, b, acc[2]);
+                acc[3] += b;
+                const double afx = a * fxr, bfy = b * fyr, g = fma(fxr, r0, fyr * r1);
+                double T = t3;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    acc[4 + k] = fma(afx, T, acc[4 + k]);
+                    acc[8 + k] = fma(bfy, T, acc[8 + k]);
+                    acc[12 + k] = fma(fxr, T, acc[12 + k]);
+                    acc[16 + k] = fma(fyr, T, acc[16 + k]);
+                    acc[31 + k] = fma(g, T, acc[31 + k]);
+                    T *= t2;
+                }
+                double q = fma(fxr, fxr, fyr * fyr) * (t3 * t3);
+#pragma unroll
+                for (int m = 0; m < 7; ++m) {
+                    acc[20 + m] += q;
+                    q *= t2;
+                }
+                acc[27] = fma(a, r0, acc[27]);
+                acc[28] = fma(b, r1, acc[28]);
+                acc[29] += r0;
+                acc[30] += r1;
+                acc[35] = fma(r0, r0, fma(r1, r1, acc[35]));
+                acc[36] += 1.0;
+            } else {
+                acc[35] += sent2;
+            }
+            return;
+        } else {
         double u, v, ju[P], jv[P];
         const uint8_t st = M::template project<true, true>(c, px, py, pz, u, v, ju, jv);
         if (st == ST_OK) {
@@ -881,6 +868,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             acc[K - 1] += 1.0;
         } else {
             acc[K - 2] += sent2;
+        }
         }
     };
     if constexpr (U == 3) {
@@ -966,7 +954,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             }
         }
     }
-    block_sum_store<K>(acc, parts + (size_t)blockIdx.x * K);
+    if constexpr (kKB) {  // expand the 37 KB sums into the NE<8> layout
+        static_assert(K == 40, "NE<8>");
+        double full[K];
+        full[0] = acc[0];
+        full[1] = acc[1];
+        full[L::B2] = acc[2];
+        full[L::B1] = acc[3];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            full[L::A_DU + k] = acc[4 + k];
+            full[L::B_DV + k] = acc[8 + k];
+            full[L::DU + k] = acc[12 + k];
+            full[L::DV + k] = acc[16 + k];
+            full[L::G + 4 + k] = acc[31 + k];
+        }
+        int t = L::DDB;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = j; k < 4; ++k, ++t) full[t] = acc[20 + j + k];
+        full[L::G + 0] = acc[27];
+        full[L::G + 1] = acc[28];
+        full[L::G + 2] = acc[29];
+        full[L::G + 3] = acc[30];
+        full[K - 2] = acc[35];
+        full[K - 1] = acc[36];
+        block_sum_store<K>(full, parts + (size_t)blockIdx.x * K);
+    } else {
+        block_sum_store<K>(acc, parts + (size_t)blockIdx.x * K);
+    }
 }
 
 // Epilogue of k_normal_eq in one launch (it was a column-sum kernel plus a
@@ -1822,14 +1839,6 @@ constexpr size_t kFusedCells = (size_t)kBlock * kFusedRMin;
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
 constexpr int kLbPatience = 512;  // polls (s_sleep between) before computing a count itself
 
-#if ACM_DIAG_SAMPLE == 7
-// Diagnostic build only: one record per tile -- wall clock (100 MHz) at
-// entry, after the first compute pass, after the look-back, after the stores
-// were issued; look-back loads, loads that found a nearer tile unpublished,
-// 64-tile windows walked, fallback (help) passes.
-constexpr size_t kDiagRecs = 1u << 18;
-__device__ unsigned long long g_sample_rec[kDiagRecs][8];
-#endif
 
 template <class TagT, int kFusedR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR >= 8 ? 3 : 6))) void k_sample_fused(CamArg cam, Grid g, size_t cells,
@@ -1870,11 +1879,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR 
     uint64_t work = tile;
     uint64_t agg = 0;
     bool published = false;
-#if ACM_DIAG_SAMPLE == 7
-    const long long d_t0 = wall_clock64();
-    long long d_t1 = 0;
-    unsigned long long d_polls = 0, d_waits = 0, d_windows = 0, d_helps = 0;
-#endif
     for (;;) {
         const size_t wbase0 = (size_t)work * kTile;
         CellWalk cw;
@@ -1884,14 +1888,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR 
             const size_t cell = wbase0 + (size_t)r * kBlock + threadIdx.x;
             bool keep = false;
             double u, v, X = 0.0, Y = 0.0, Z = 0.0;
-#if ACM_DIAG_SAMPLE == 2 || ACM_DIAG_SAMPLE == 3 || ACM_DIAG_SAMPLE == 6  // no unprojection
-            u = ((double)cw.j + 0.5) * g.cw;
-            v = ((double)cw.i + 0.5) * g.ch;
-            X = u; Y = v; Z = 1.0;
-            keep = cell < cells && (cw.i + cw.j) % 16 != 0;
-#else
             if (cell < cells) keep = sample_cell<TagT>(c, g, cw, u, v, X, Y, Z);
-#endif
             const uint64_t mr = __ballot(keep);
             if (lane == 0) {
                 sm[r][wid] = (uint32_t)__popcll(mr);
@@ -1920,25 +1917,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR 
             s_lb_helped |= 1ull << l;
         }
         __syncthreads();
-#if ACM_DIAG_SAMPLE == 7
-        if (d_t1 == 0) d_t1 = wall_clock64();
-#endif
         // Decoupled look-back by wave 0.  A predecessor that has not
         // published after g.patience polls is counted here by the whole
         // workgroup (next pass of the loop); then this tile is recomputed.
-#if ACM_DIAG_SAMPLE == 6  // diagnostic: no look-back at all (wrong offsets; timing only)
-        if (threadIdx.x == 0) s_lb_state = 1;
-        __syncthreads();
-#endif
-#if ACM_DIAG_SAMPLE == 8  // diagnostic: full compute and stores, no look-back: each
-        // tile writes at 15/16 of its cell offset (in bounds: the outputs hold
-        // one slot per cell; wrong offsets, timing only)
-        if (threadIdx.x == 0) {
-            s_lb_excl = tile * kTile - (tile * kTile) / 16;
-            s_lb_state = 1;
-        }
-        __syncthreads();
-#endif
         if (wid == 0 && __builtin_amdgcn_readfirstlane(s_lb_state) == 0) {
             int64_t top = (int64_t)s_lb_top;
             uint64_t excl = s_lb_excl, helped = s_lb_helped;
@@ -1949,17 +1930,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR 
                                                           __HIP_MEMORY_SCOPE_AGENT)
                                       : kLbIncl;  // before tile 0: prefix 0
                 if (((helped >> lane) & 1ull) && (w >> 62) == 0) w = help_w;
-#if ACM_DIAG_SAMPLE == 7
-                ++d_polls;
-#endif
                 const uint64_t incl = __ballot((w >> 62) == 2);
                 const uint64_t none = __ballot((w >> 62) == 0);
                 const int stop = incl ? __ffsll((long long)incl) - 1 : 64;
                 const uint64_t need = stop == 63 || stop == 64 ? ~0ull : ((2ull << stop) - 1);
                 if (none & need) {  // a nearer tile has not published yet
-#if ACM_DIAG_SAMPLE == 7
-                    ++d_waits;
-#endif
                     if (++polls < g.patience) {
                         __builtin_amdgcn_s_sleep(2);
                         continue;
@@ -1992,18 +1967,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR 
                 top -= 64;
                 helped = 0;
                 polls = 0;
-#if ACM_DIAG_SAMPLE == 7
-                ++d_windows;
-#endif
             }
         }
         __syncthreads();
         const int state = __builtin_amdgcn_readfirstlane(s_lb_state);
         if (state == 1 && work == tile) break;  // prefix known, own rays in registers
         if (state == 2) {
-#if ACM_DIAG_SAMPLE == 7
-            ++d_helps;
-#endif
             work = s_lb_top - s_lb_help;
             __syncthreads();  // everyone has read the request before it is reset
             if (threadIdx.x == 0) s_lb_state = 0;
@@ -2019,9 +1988,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR 
         }
     }
     __syncthreads();
-#if ACM_DIAG_SAMPLE == 7
-    const long long d_t2 = wall_clock64();
-#endif
     uint64_t run = s_excl;
     CellWalk cw;
     cw.init(g, base, threadIdx.x);
@@ -2035,13 +2001,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR 
         const uint64_t mr = s_mask[r][wid];
         const uint32_t rank = (uint32_t)__popcll(mr & below);
         const uint32_t cnt = (uint32_t)__popcll(mr);
-#if ACM_DIAG_SAMPLE == 1 || ACM_DIAG_SAMPLE == 3 || ACM_DIAG_SAMPLE == 6  // no output stores
-        (void)rank;
-        (void)cnt;
-        if (((mr >> lane) & 1ull) && s_ray[r][wid][0] == 1234.5) {
-            st2<false>(uv_out, 0.0, 0.0);
-        }
-#else
         if ((mr >> lane) & 1ull) {
             // the same u, v as sample_cell (point_sampling.rs:69-70): 16 B per
             // lane, consecutive kept points -> one contiguous run per wave
@@ -2065,22 +2024,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR 
             if (lane == 0 && h) dst[0] = lx[0];
             if (lane == 63 && ((nd - h) & 1u)) dst[nd - 1] = lx[nd - 1];
         }
-#endif
         run += tot;
     }
-#if ACM_DIAG_SAMPLE == 7
-    if (threadIdx.x == 0 && tile < kDiagRecs) {
-        unsigned long long* rec = g_sample_rec[tile];
-        rec[0] = d_t0;
-        rec[1] = d_t1;
-        rec[2] = d_t2;
-        rec[3] = wall_clock64();
-        rec[4] = d_polls;
-        rec[5] = d_waits;
-        rec[6] = d_windows;
-        rec[7] = d_helps;
-    }
-#endif
 }
 
 // ----------------------------------------------------------------- median
@@ -2999,13 +2944,6 @@ using namespace acm;
 
 // ====================================================================== C-ABI
 extern "C" {
-#if ACM_DIAG_SAMPLE == 7
-ACM_API int acm_diag_sample_records(void* host, size_t bytes) {
-    if (bytes > sizeof(g_sample_rec)) bytes = sizeof(g_sample_rec);
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sample_rec), bytes, 0,
-                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
-}
-#endif
 
 ACM_API int acm_num_params(int model) {
     switch (model) {
@@ -3194,17 +3132,6 @@ ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_
         const dim3 g(grid_for(n)), b(kBlock);
         const bool nt = n * 25 > kNtThresholdBytes;  // rays + status written once
         const bool ntl = g_nt_loads_unproject == 1;
-#ifdef ACM_DIAG_REFILL
-        if (std::is_same<TagT, Tag<RadTan>>::value && layout == ACM_LAYOUT_AOS) {
-            auto kern = k_unproject_refill<ACM_DIAG_REFILL>;
-            const size_t waves = (size_t)resident_blocks((const void*)kern) * (kBlock / 64);
-            const size_t chunk = (n + waves - 1) / waves;
-            const size_t blocks = ((n + chunk - 1) / chunk + kBlock / 64 - 1) / (kBlock / 64);
-            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), b, 0, s, prep(*cam, refn), n, chunk,
-                               points_2d, rays, status);
-            return check_launch("acm_unproject");
-        }
-#endif
         // knob: -1 auto = 2 pixels per lane, AoS stores LDS-staged per
         // UnprojectStaged; 1 / 2 = pixels per lane with three 8-B stores per
         // AoS ray; 3 = 1 pixel per lane with LDS-staged stores
@@ -3946,12 +3873,6 @@ ACM_API const char* acm_version(void) {
     return "acm 0.3.0 (gfx950"
 #ifdef ACM_IEEE_MATH
            "; ACM_IEEE_MATH"
-#endif
-#ifdef ACM_DIAG_SAMPLE
-           "; ACM_DIAG_SAMPLE"
-#endif
-#ifdef ACM_DIAG_REFILL
-           "; ACM_DIAG_REFILL"
 #endif
            ")";
 }

@@ -360,8 +360,9 @@ struct RadTan {
         return st;
     }
     // rad_tan.rs:401-524: Newton on the 2x2 distortion Jacobian, <=100 steps,
-    // split into init / step / finish so a lane-refill kernel can run the
-    // same per-point iterates (k_unproject_refill); unproject() chains them.
+    // split into init / step / finish (the round-2 lane-refill experiment ran
+    // the same per-point iterates from them); unproject() chains
+    // them.
     struct Newton {
         T tx, ty, px, py;
         unsigned it;
@@ -602,6 +603,59 @@ struct KannalaBrandt {
             jv[0] = T(0); jv[1] = theta_d * y_r; jv[2] = T(0); jv[3] = T(1);
             jv[4] = fyr * theta3; jv[5] = fyr * theta5; jv[6] = fyr * theta7; jv[7] = fyr * theta9;
         }
+        return st;
+    }
+    // The fused normal equations' view of project<true, true> (FAST): the
+    // same u, v and status, and instead of the 2 x 8 Jacobian the scalars it
+    // is built from -- a = theta_d x_r (du/dfx), b = theta_d y_r (dv/dfy),
+    // fx x_r, fy y_r, theta^2, theta^3 -- since du/dk_i = fx x_r
+    // theta^(2i+1) and dv/dk_i = fy y_r theta^(2i+1) (kannala_brandt.rs:
+    // 367-390): k_normal_eq then accumulates the distortion block from
+    // powers of theta on the fly instead of holding 16 Jacobian entries.
+    __device__ static __forceinline__ uint8_t project_ne(const Cam<T>& c, T x, T y, T z, T& u,
+                                                         T& v, T& a, T& b, T& fxr, T& fyr,
+                                                         T& th2, T& th3) {
+        // the FAST form of project() above, operation for operation
+        const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
+        const T k1 = c.p[4], k2 = c.p[5], k3 = c.p[6], k4 = c.p[7];
+        const uint8_t st = z < T(0) ? ST_POINT_IS_OUT_SIDE_IMAGE
+                                    : (z < T(kEps) ? ST_POINT_AT_CAMERA_CENTER : ST_OK);
+        const T r2 = x * x + y * y;
+        T r, theta, ir;
+        bool axis;
+#ifndef ACM_IEEE_MATH
+        if (nr_range(r2) && nr_range(z) && z < T(INFINITY)) {
+            ir = rsq_nr(r2);
+            r = r2 * ir;
+            const bool swap = r > z;
+            const T q = swap ? z * ir : r * rcp_nr(z);
+            const T at = atan01(q);
+            theta = swap ? T(1.5707963267948966) - at : at;
+        } else {
+            r = sqrt(r2);
+            theta = atan2_ge0(r, z);
+            ir = T(1) / r;
+        }
+        axis = false;
+        if (r2 < T(1e-30)) axis = sqrt(r2) < T(kEps);
+#else
+        r = sqrt(r2);
+        theta = atan2_ge0(r, z);
+        axis = r < T(kEps);
+        ir = T(1) / r;
+#endif
+        th2 = theta * theta;
+        th3 = th2 * theta;
+        const T theta5 = th3 * th2, theta7 = theta5 * th2, theta9 = theta7 * th2;
+        const T theta_d = theta + k1 * th3 + k2 * theta5 + k3 * theta7 + k4 * theta9;
+        const T x_r = axis ? T(0) : x * ir;
+        const T y_r = axis ? T(0) : y * ir;
+        u = fx * theta_d * x_r + cx;
+        v = fy * theta_d * y_r + cy;
+        a = theta_d * x_r;
+        b = theta_d * y_r;
+        fxr = fx * x_r;
+        fyr = fy * y_r;
         return st;
     }
     // Certified fast Newton (double only).  The reference's loop

@@ -125,7 +125,10 @@ def config3_ne_all(n):
             factors.KannalaBrandtCameraParamsFactor, factors.DoubleSphereCameraParamsFactor,
             factors.UcmCameraParamsFactor, factors.EucmCameraParamsFactor,
             factors.FovCameraParamsFactor]
+    only = os.environ.get("NE_MODELS")  # e.g. "2": restrict the sweep
     for mid, fcls in enumerate(facs):
+        if only and str(mid) not in only.split(","):
+            continue
         params, (w, h) = samples.SAMPLES[mid]
         m = fcls.MODEL._from_params(list(params), Resolution(w, h))
         uv, _, _ = m.project_batch(pts)

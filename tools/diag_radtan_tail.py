@@ -1,0 +1,81 @@
+"""RadTan unproject on BASELINE config 4's own pixels (6.25M synthetic points
+projected by the sample camera, NaN for failed projections): where does the
+time go?  Times acm_unproject on (a) all pixels, (b) the finite ones, (c) the
+finite ones minus the ~0.01% whose reference Newton loop never converges
+(100 steps, NumericalError), each resized to the same count by repeating,
+plus the fraction of such pixels and of 128-pixel waves holding one.
+
+  python tools/diag_radtan_tail.py [--points N]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "apex-camera-models_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=6_250_000)
+    a = ap.parse_args()
+    import torch
+    from apex_camera_models import _lib, samples
+    from apex_camera_models.camera import MODEL_CLASSES, Resolution
+    L = _lib.load()
+    params, (w, h) = samples.SAMPLES[1]
+    m = MODEL_CLASSES["rad_tan"]._from_params(list(params), Resolution(w, h))
+    n = a.points
+    pts = samples.synthetic_points_device(n, offset=3 * n)
+    uv, st, _ = m.project_batch(pts)
+    cam = m.acm_camera()
+    sh = torch.cuda.current_stream().cuda_stream
+
+    def timed(px, flag=0):
+        k = px.shape[0]
+        ray = torch.empty((k, 3), dtype=torch.float64, device="cuda")
+        s2 = torch.empty((k,), dtype=torch.uint8, device="cuda")
+        for _ in range(3):
+            L.acm_unproject(ctypes.byref(cam), k, px.data_ptr(), ray.data_ptr(), flag,
+                            s2.data_ptr(), sh)
+        torch.cuda.synchronize()
+        best = 1e9
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                L.acm_unproject(ctypes.byref(cam), k, px.data_ptr(), ray.data_ptr(), flag,
+                                s2.data_ptr(), sh)
+            e1.record()
+            torch.cuda.synchronize()
+            best = min(best, e0.elapsed_time(e1) / 5)
+        return best, s2
+
+    def fill(px):  # repeat to n pixels
+        r = (n + px.shape[0] - 1) // px.shape[0]
+        return px.repeat(r, 1)[:n].contiguous()
+
+    t_all, s_all = timed(uv)
+    fin = torch.isfinite(uv).all(1)
+    px_f = fill(uv[fin])
+    t_fin, s_fin = timed(px_f)
+    bad = s_fin == 4
+    px_c = fill(px_f[~bad])
+    t_conv, _ = timed(px_c)
+    waves = bad[: (n // 128) * 128].reshape(-1, 128).any(1).float().mean().item()
+    gb = 41 * n / 1e9
+    print(json.dumps({
+        "what": "RadTan unproject on config-4 pixels", "points": n,
+        "nan_fraction": float((~fin).float().mean()),
+        "nonconverging_fraction_of_finite": float(bad.float().mean()),
+        "waves128_with_nonconverging": waves,
+        "ms_all": round(t_all, 4), "TBps_all": round(gb / t_all, 2),
+        "ms_finite": round(t_fin, 4), "TBps_finite": round(gb / t_fin, 2),
+        "ms_converging": round(t_conv, 4), "TBps_converging": round(gb / t_conv, 2)}))
+
+
+if __name__ == "__main__":
+    main()
