@@ -1731,7 +1731,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_count(CamArg cam, Grid g, size_t
 // ballot their rank, each writes its 16-B pixel at offset + rank, and the
 // compacted rays (3 * kept doubles, staged in the wave's 1.5 KiB of LDS) go
 // out as 16-B pieces.  A segment whose count is 0 is skipped.
-template <class TagT, int SPW, bool ILV>
+template <class TagT, int SPW, bool ILV, bool NT = false>
 __global__ __launch_bounds__(kBlock) void k_seg_write(CamArg cam, Grid g, size_t cells,
                                                       const uint32_t* __restrict__ seg_cnt,
                                                       const uint64_t* __restrict__ blk_off,
@@ -1788,7 +1788,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(CamArg cam, Grid g, size_t
         const uint64_t m = __ballot(keep);
         const uint32_t rank = (uint32_t)__popcll(m & below);
         if (keep) {
-            st2<false>(uv_out + 2 * (off + rank), u, v);  // 16 B per lane, one run per wave
+            st2<NT>(uv_out + 2 * (off + rank), u, v);  // 16 B per lane, one run per wave
             double* d = lx + 3 * rank;
             d[0] = X;
             d[1] = Y;
@@ -1806,7 +1806,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(CamArg cam, Grid g, size_t
         const uint32_t np = (nd - h) >> 1;
         for (uint32_t p = lane; p < np; p += 64) {
             const uint32_t dd = h + 2 * p;
-            st2<false>(dst + dd, lx[dd], lx[dd + 1]);
+            st2<NT>(dst + dd, lx[dd], lx[dd + 1]);
         }
         if (lane == 0 && h) dst[0] = lx[0];
         if (lane == 63 && ((nd - h) & 1u)) dst[nd - 1] = lx[nd - 1];
@@ -2493,7 +2493,9 @@ __global__ __launch_bounds__(kBlock) void k_tsqr_final(const double* __restrict_
 // its running sum follows the reference's serial point order within the
 // chunk and no cross-lane reduction is needed.  The per-w constants come
 // from a host-built table (w, 2 tan(w/2), 2 tan(w/2)/w) so tan is glibc's.
-// Compute-bound: one f64 atan2 + 2 div + sqrt per (point, w).
+// Compute-bound: one f64 atan (degree-20 polynomial) + rsq-based sqrt per
+// (point, w); every per-point quantity (r / z, z / r, 1 / r, fx x, cx - u,
+// ...) is computed once in LDS and shared by the 290 grid lanes.
 constexpr int kFovGrid = ACM_FOV_GRID_SIZE;
 constexpr int kFovBlock = 320;
 constexpr int kFovMaxBlocks = 2048;
@@ -2517,8 +2519,8 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n
                                                         double* __restrict__ parts) {
     __shared__ double sx[kFovBlock], sy[kFovBlock], sz[kFovBlock], su[kFovBlock],
         sv[kFovBlock], sr2[kFovBlock], sr[kFovBlock], stz[kFovBlock], szt[kFovBlock],
-        sir[kFovBlock];
-    __shared__ unsigned char sfast[kFovBlock];
+        sir[kFovBlock], sax[kFovBlock], say[kFovBlock], sbx[kFovBlock], sby[kFovBlock];
+    __shared__ unsigned char smode[kFovBlock];
     const int t = threadIdx.x;
     const bool active = t < kFovGrid;
     const double fx = cam.params[0], fy = cam.params[1], cx = cam.params[2], cy = cam.params[3];
@@ -2540,36 +2542,54 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n
             load_point<LAYOUT>(pts, n, i, x, y, z);
             const double r2 = x * x + y * y;  // :192-193
             const double r = sqrt(r2);
+            const double u0 = obs[2 * i], v0 = obs[2 * i + 1];
             sx[t] = x; sy[t] = y; sz[t] = z;
-            su[t] = obs[2 * i]; sv[t] = obs[2 * i + 1];
+            su[t] = u0; sv[t] = v0;
             sr2[t] = r2; sr[t] = r;
-            // z > 0, r > 0, both finite: atan2(2 tan(w/2) r, z) = atan(2 tan(w/2) r / z)
-            // from per-point r/z, z/r, 1/r shared by every grid lane
+            // mode 0: z > 0, r > 0, both finite -- atan2(2 tan(w/2) r, z) =
+            // atan(2 tan(w/2) r / z) from per-point r/z, z/r, 1/r shared by
+            // every grid lane; 1: r2 < sqrt(EPS) (rd = rd0, :200-205);
+            // 2: anything else (OCML atan2, fov_rd_general)
             const bool fast = z > 0.0 && r > 0.0 && z < INFINITY && r < INFINITY;
-            sfast[t] = fast;
+            smode[t] = r2 < kEpsSqrt ? 1 : (fast ? 0 : 2);
             stz[t] = fast ? r / z : 0.0;
             szt[t] = fast ? z / r : 0.0;
             sir[t] = fast ? 1.0 / r : 0.0;
+            // the error terms as fma(fx x, rd, cx - u) / fma(fy y, rd, cy - v):
+            // the reference's (fx (x rd) + cx) - u up to the last bit (the
+            // grid sums are held to 1e-12, not to the serial order)
+            sax[t] = fx * x; say[t] = fy * y;
+            sbx[t] = cx - u0; sby[t] = cy - v0;
         }
         __syncthreads();
         const int m = (int)(b1 - base < (size_t)kFovBlock ? b1 - base : (size_t)kFovBlock);
         auto eval = [&](int k) -> double {
-            const double x = sx[k], y = sy[k], r2 = sr2[k];
-            double rd;
-            if (sfast[k]) {  // uniform: every lane reads point k
-                // a = 2 tan(w/2) r / z; atan(a) = pi/2 - atan(1/a) above 1
-                const double a = tw2 * stz[k];
-                const bool big = a > 1.0;
-                const double at = atan01(big ? itw2 * szt[k] : a);
-                const double atan_wrd = big ? 1.5707963267948966 - at : at;      // :196
-                rd = r2 < kEpsSqrt ? rd0 : atan_wrd * sir[k] * iw;                // :200-205
+            const int md = smode[k];  // uniform: every lane reads point k
+            double du, dv;
+            if (md != 2) {
+                double rd;
+                if (md == 0) {
+                    // a = 2 tan(w/2) r / z; atan(a) = pi/2 - atan(1/a) above 1
+                    const double a = tw2 * stz[k];
+                    const bool big = a > 1.0;
+                    const double at = atan01(big ? itw2 * szt[k] : a);
+                    const double atan_wrd = big ? 1.5707963267948966 - at : at;  // :196
+                    rd = atan_wrd * sir[k] * iw;                                  // :205
+                } else {
+                    rd = rd0;  // :200-203
+                }
+                du = fma(sax[k], rd, sbx[k]);
+                dv = fma(say[k], rd, sby[k]);
             } else {
-                rd = fov_rd_general(tw2, sr[k], sz[k], w, r2, rd0);
+                const double rd = fov_rd_general(tw2, sr[k], sz[k], w, sr2[k], rd0);
+                const double mx = sx[k] * rd, my = sy[k] * rd;
+                du = (fx * mx + cx) - su[k];
+                dv = (fy * my + cy) - sv[k];
             }
-            const double mx = x * rd, my = y * rd;
-            const double du = (fx * mx + cx) - su[k];
-            const double dv = (fy * my + cy) - sv[k];
-            return sqrt(du * du + dv * dv);  // :211-213
+            // sqrt(du^2 + dv^2) (:211-213) from rsq + Newton (~1 ulp) on the
+            // normal range, the IEEE sqrt elsewhere (0, huge, NaN)
+            const double d2 = fma(du, du, dv * dv);
+            return nr_range(d2) ? d2 * rsq_nr(d2) : sqrt(d2);
         };
         if (active) {
             int k = 0;
@@ -3491,15 +3511,22 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
                                counts, (uint64_t)cells);
             // ACM_TUNE_SAMPLE_WRITE: segments per write wave and order
             // (-1 auto = 16 interleaved; 1 = 64 contiguous, 2 = 16
-            // interleaved, 3 = 4 interleaved, 4 = 16 contiguous)
+            // interleaved, 3 = 4 interleaved, 4 = 16 contiguous, 5 = 16
+            // interleaved with non-temporal stores)
+            // auto: 4 segments per wave for the cheapest unprojections (UCM,
+            // EUCM, FOV: 0.71 vs 0.84 ms at 1e8 cells), 16 for the rest (KB
+            // 0.82 vs 0.95, DS 0.81 vs 0.86; profiles/r03f_diag_sample.log)
             const int wv0 = g_sample_write.load(std::memory_order_relaxed);
-            const int wv = wv0 < 0 ? 2 : wv0;
+            const bool cheap = cam->model == ACM_UCM || cam->model == ACM_EUCM ||
+                               cam->model == ACM_FOV;
+            const int wv = wv0 < 0 ? (cheap ? 3 : 2) : wv0;
             auto wlaunch = [&](auto kern, int spw) {
                 const size_t nwb = (nseg + 4 * (size_t)spw - 1) / (4 * (size_t)spw);
                 hipLaunchKernelGGL(kern, dim3((unsigned)nwb), dim3(kBlock), 0, s, ca, g, cells,
                                    seg_cnt, blk_off, points_2d_out, points_3d_out);
             };
-            if (wv == 1) wlaunch(k_seg_write<TagT, 64, false>, 64);
+            if (wv == 5) wlaunch(k_seg_write<TagT, 16, true, true>, 16);
+            else if (wv == 1) wlaunch(k_seg_write<TagT, 64, false>, 64);
             else if (wv == 3) wlaunch(k_seg_write<TagT, 4, true>, 4);
             else if (wv == 4) wlaunch(k_seg_write<TagT, 16, false>, 16);
             else wlaunch(k_seg_write<TagT, 16, true>, 16);
@@ -3845,7 +3872,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_UNPROJECT_RCP, &g_unproject_rcp, -1, 1, "value must be -1..1"},
         {ACM_TUNE_SAMPLE_PATIENCE, &g_sample_patience, -1, 1 << 20, "value must be -1..2^20"},
         {ACM_TUNE_SAMPLE_CERT, &g_sample_cert, -1, 0, "value must be -1 (auto) or 0"},
-        {ACM_TUNE_SAMPLE_WRITE, &g_sample_write, -1, 4, "value must be -1..4"},
+        {ACM_TUNE_SAMPLE_WRITE, &g_sample_write, -1, 5, "value must be -1..5"},
         {ACM_TUNE_UNPROJECT_PPT, &g_unproject_ppt, -1, 3, "value must be -1..3"},
     };
     if (key == ACM_TUNE_NEWTON_FAST)  // removed (r03): numerics are chosen per call

@@ -155,3 +155,58 @@ def test_certified_counts_equal_cell_by_cell_counts_random_cameras():
                 assert np.array_equal(uv1.cpu().numpy(), uvo), (t, params)
     finally:
         L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, -1)
+
+
+# random cameras of the closed-form models whose keep boundaries fall inside
+# the image: DS with alpha > 0.5 (r2 > 1 / (2 alpha - 1) rejected) and xi < 0
+# (pz = coeff mz - xi crossing 0 is not possible then, but denom = mz^2 + r2
+# small is), UCM / EUCM with alpha > 0.5 (their r2 conditions), FOV with a
+# wide w (rd w near pi/2) and short focal lengths
+def _random_closed_form(model, rng):
+    w, h = int(rng.integers(300, 900)), int(rng.integers(240, 700))
+    f = rng.uniform(0.15, 0.6) * w
+    base = [f, f * rng.uniform(0.9, 1.1), w * rng.uniform(0.2, 0.8), h * rng.uniform(0.2, 0.8)]
+    if model == 0:
+        extra = []
+    elif model == 3:  # DS: alpha in (0, 1], xi in [-1, 1]
+        extra = [rng.uniform(0.3, 1.0), rng.uniform(-1.0, 1.0)]
+    elif model == 4:  # UCM: alpha around 0.5 .. 1.2
+        extra = [rng.uniform(0.3, 1.2)]
+    elif model == 5:  # EUCM: alpha, beta
+        extra = [rng.uniform(0.3, 1.0), rng.uniform(0.3, 2.5)]
+    else:  # FOV: w up to ~2.9
+        extra = [rng.uniform(0.3, 2.9)]
+    return base + extra, w, h
+
+
+@pytest.mark.parametrize("model", [0, 3, 4, 5, 6])
+def test_interval_certificates_equal_cell_by_cell_random_cameras(model):
+    """The device interval certificates (seg_keep_iv) against counting every
+    cell (ACM_TUNE_SAMPLE_CERT = 0) and against the oracle: same kept set, same
+    order, bit-identical outputs, for 30 random cameras per model whose keep
+    boundaries cross the image."""
+    import torch
+    from apex_camera_models import _lib, util
+    from apex_camera_models.camera import MODEL_CLASSES, Resolution
+    names = {0: "pinhole", 3: "double_sphere", 4: "ucm", 5: "eucm", 6: "fov"}
+    L = _lib.load()
+    rng = np.random.default_rng(100 + model)
+    dropped_somewhere = 0
+    try:
+        for t in range(30):
+            params, w, h = _random_closed_form(model, rng)
+            m = MODEL_CLASSES[names[model]]._from_params(params, Resolution(w, h))
+            n = 120_000
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, -1)
+            uv1, xyz1 = util.sample_points(m, n)
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, 0)
+            uv0, xyz0 = util.sample_points(m, n)
+            assert torch.equal(uv1, uv0) and torch.equal(xyz1.view(torch.int64),
+                                                         xyz0.view(torch.int64)), (t, params)
+            uvo, xyzo, total = O.sample_points(model, params, w, h, n)
+            assert np.array_equal(uv1.cpu().numpy(), uvo), (t, params)
+            dropped_somewhere += int(uvo.shape[0] < total)
+    finally:
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, -1)
+    if model in (3, 4, 5):  # (Pinhole and FOV keep every in-image cell)
+        assert dropped_somewhere >= 5  # the boundaries really were inside the image
