@@ -1,7 +1,7 @@
 """Driver for the counter passes of the kernels DESIGN.md calls FP64-VALU
 bound: RadTan and KB unproject (10M pixels), KB fused
 normal equations (10M points), the FOV grid search (9.3M KB-sampled
-correspondences) and the fused sample_points (1e8-cell KB grid).  Each runs
+correspondences) and sample_points (1e8-cell KB grid, the default segment path).  Each runs
 `--reps` times after one warm-up; the HIP-event time per call is printed as
 one JSON line per kernel, so the same command under `rocprofv3 --pmc ...`
 yields per-dispatch counters and the event times side by side.
@@ -28,9 +28,9 @@ def main():
     ap.add_argument("--points", type=int, default=10_000_000)
     ap.add_argument("--cells", type=int, default=100_000_000)
     ap.add_argument("--sample-fused", type=int, default=None,
-                    help="ACM_TUNE_SAMPLE_FUSED for sample_kb (-1 auto, 0 two-pass, 1/2/3 = R 4/8/16)")
-    ap.add_argument("--lib", default=None, help="load this libacm build instead (diagnostic "
-                    "builds: make -C apex-camera-models_amd diag)")
+                    help="ACM_TUNE_SAMPLE_FUSED for sample_kb (-1 auto = segment path, 0 two-pass, 1/2/3 = single pass R 2/4/8)")
+    ap.add_argument("--lib", default=None, help="load this libacm build instead (A/B builds, "
+                    "e.g. make -C apex-camera-models_amd ieee)")
     a = ap.parse_args()
     want = set(a.only.split(","))
     if a.lib:
