@@ -134,7 +134,7 @@ __host__ __device__ inline void unproject_consts(int model, const T* p, T* uk) {
 struct CamArg : acm_camera {
     double ifx, ify;
     double uk[4];
-    double kc[9];  // KB sample_points: certified kept interval + initial guess (Cam::kc)
+    double kc[12];  // KB sample_points: certified kept interval + initial guess (Cam::kc)
 };
 
 template <class T>
@@ -149,7 +149,7 @@ __device__ __forceinline__ Cam<T> make_cam(const acm_camera& c) {
     k.ifx = k.ify = T(0);  // divide
     unproject_consts<T>(c.model, k.p, k.uk);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) k.kc[i] = T(0);
+    for (int i = 0; i < 12; ++i) k.kc[i] = T(0);
     k.kc[0] = T(INFINITY);  // no certified interval (sample_points only)
     return k;
 }
@@ -169,7 +169,7 @@ __device__ __forceinline__ Cam<T> make_cam(const CamArg& c) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) k.uk[i] = c.uk[i];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) k.kc[i] = c.kc[i];
+    for (int i = 0; i < 12; ++i) k.kc[i] = c.kc[i];
     return k;
 }
 
@@ -1481,9 +1481,9 @@ enum : int { SEG_UNKNOWN = 0, SEG_ALL = 1, SEG_NONE = 2 };
 // (ACM_TUNE_SAMPLE_CERT = 0): every segment is decided cell by cell.
 struct SegCert {
     int on;
-    int ig_ok;  // KB: ig[] fits theta*(ru) on [0, all_hi] well enough for ray_certified
+    int ig_ok;  // KB: ig[] fits theta*(ru) on [0, all_hi] for ray_certified: its Newton steps (1, 2) or 0
     double all_lo, all_hi, none_lo, none_hi;
-    double ig[7];  // KB: theta*(ru) ~= ru * sum ig[i] ru^(2i)
+    double ig[9];  // KB: theta*(ru) ~= ru * sum ig[i] ru^(2i)
 };
 
 // Rigorous bounds of r2 = mx^2 + my^2 over the cells [c0, c1] (inclusive,
@@ -2730,7 +2730,7 @@ static CamArg prep(acm_camera c, bool reference_newton = false) {
     if (reference_newton &&
         (c.model == ACM_KANNALA_BRANDT || c.model == ACM_RADTAN || c.model == ACM_FOV))
         a.uk[0] = NAN;  // fast Newton loops / FOV fast unprojection off
-    for (int i = 0; i < 9; ++i) a.kc[i] = 0.0;
+    for (int i = 0; i < 12; ++i) a.kc[i] = 0.0;
     a.kc[0] = INFINITY;  // no certified interval (set by acm_sample_points_ex for KB)
     return a;
 }
@@ -2832,11 +2832,12 @@ static SegCert kb_seg_cert_on(const double* p, double tmax) {
 // then counted cell by cell.  The theta range the bounds cover is tried at a
 // few sizes (a strongly distorted camera's f' may vanish near theta = 2 but
 // not below pi/2); the certificate covering the most is kept.
-// KB: theta*(ru) ~= ru g(ru^2), g the degree-6 interpolant of theta*(ru)/ru
+// KB: theta*(ru) ~= ru g(ru^2), g the degree-8 interpolant of theta*(ru)/ru
 // in s = ru^2 at Chebyshev nodes on [0, all_hi^2] (theta* solved in long
-// double).  Accepted for ray_certified only if, over 4001 points of the
-// interval, the error e0 keeps two Newton steps exact to ~1e-13
-// (M^3 e0^4 <= 1e-13, M as in kb_seg_cert_on) and below 1e-5.
+// double).  Over 4001 points of the interval its error e0 decides
+// ray_certified's Newton steps: one when M e0^2 <= 1e-17 (M as in
+// kb_seg_cert_on), two when M^3 e0^4 <= 1e-13 and e0 <= 1e-5, else the fit
+// is not used (ig_ok = 0).
 static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
     s.ig_ok = 0;
     const long double k1 = p[4], k2 = p[5], k3 = p[6], k4 = p[7];
@@ -2854,7 +2855,7 @@ static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
     };
     const double R = s.all_hi;
     if (!(R > 1e-3)) return;
-    constexpr int N = 7;
+    constexpr int N = 9;
     long double A[N][N + 1];
     const long double S = (long double)R * R;
     for (int j = 0; j < N; ++j) {
@@ -2885,7 +2886,7 @@ static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
         for (int k = N - 2; k >= 0; --k) g = std::fma(g, ru * ru, s.ig[k]);
         e0 = std::fmax(e0, std::fabs((double)((long double)ru * g - root(ru))));
     }
-    s.ig_ok = e0 <= 1e-5 && M * M * M * e0 * e0 * e0 * e0 <= 1e-13;
+    s.ig_ok = M * e0 * e0 <= 1e-17 ? 1 : (e0 <= 1e-5 && M * M * M * e0 * e0 * e0 * e0 <= 1e-13 ? 2 : 0);
 }
 
 static SegCert kb_seg_cert(const double* p) {
@@ -3480,7 +3481,8 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
         if (kc.on && kc.ig_ok && kc.all_hi > kc.all_lo) {
             ca.kc[0] = kc.all_lo;
             ca.kc[1] = kc.all_hi;
-            for (int i = 0; i < 7; ++i) ca.kc[2 + i] = kc.ig[i];
+            ca.kc[2] = kc.ig_ok;  // Newton steps of ray_certified
+            for (int i = 0; i < 9; ++i) ca.kc[3 + i] = kc.ig[i];
         }
     }
     if (!cells) {  // nothing to launch: counts = [0 kept, 0 cells]

@@ -199,6 +199,19 @@ __device__ __forceinline__ void sincos_0_2(double t, double* sn, double* cs) {
     sincos(t, sn, cs);
 }
 __device__ __forceinline__ void sincos_0_2(float t, float* sn, float* cs) { sincosf(t, sn, cs); }
+// The same polynomials without the OCML fallback, for a caller that knows
+// t is in [0, 2] (KannalaBrandt::ray_certified: theta in [0, pi/2)).
+__device__ __forceinline__ void sincos_poly_0_2(double t, double* sn, double* cs) {
+    const double s = t * t;
+    double ps = kSinS[10], pc = kCosC[10];
+#pragma unroll
+    for (int k = 9; k >= 0; --k) {
+        ps = fma(ps, s, kSinS[k]);
+        pc = fma(pc, s, kCosC[k]);
+    }
+    *sn = t * ps;
+    *cs = pc;
+}
 
 // ------------------------------------------- division by a shared divisor
 // RN(a / b) from y = RN(1 / b) (one IEEE division) and two FMAs: q = RN(a*y)
@@ -265,8 +278,9 @@ struct Cam {
     T uk[4];
     // KB sample_points (kc[1] > 0 only there): cells whose ru lies in the
     // host-certified kept interval [kc[0], kc[1]] (acm.hip kb_seg_cert) take
-    // KannalaBrandt::ray_certified; kc[2..8] = the initial-guess polynomial.
-    T kc[9];
+    // KannalaBrandt::ray_certified; kc[2] = its Newton steps (1 or 2),
+    // kc[3..11] = the initial-guess polynomial.
+    T kc[12];
 };
 
 // (u - cx) / fx with fx uniform: RN(a / b) from the host's RN(1 / b) and the
@@ -744,22 +758,26 @@ struct KannalaBrandt {
     // the status and the keep decision are known, and the ray is held to
     // 1e-10, so theta need not follow the reference's iterates -- only be
     // accurate.  The reference stops at |delta| < 1e-6, i.e. within ~M 1e-12
-    // of the root theta* (kb_seg_cert's bound); here theta_0 = ru P(ru^2),
-    // the host's fit of theta*(ru) (error <= 1e-5, checked on the host), then
-    // two Newton steps (error <= M^3 1e-20): theta* to rounding.  1 / ru
-    // from rsq; ru < pi/2 (the certified interval ends below the clamp).
+    // of the root theta* (kb_seg_cert's bound); here theta_0 = ru g(ru^2),
+    // the host's fit of theta*(ru) (its error e0 measured on the host), then
+    // kc[2] Newton steps -- one when M e0^2 is already at rounding level,
+    // else two (M^3 e0^4 <= 1e-13).  1 / ru from rsq.  The certified interval
+    // ends below the clamp (ru = |m| < pi/2), so (sin(theta) m / ru,
+    // cos(theta)) is a unit vector up to rounding (sin^2 + cos^2 = 1): no
+    // normalisation -- within a few ulp of the reference's normalised ray.
     __device__ static __forceinline__ void ray_certified(const Cam<T>& c, T mx, T my, T r2, T& X,
                                                          T& Y, T& Z) {
         const T k1 = c.p[4], k2 = c.p[5], k3 = c.p[6], k4 = c.p[7];
         const T ir = rsq_nr(r2);
         const T ru = r2 * ir;
         const T s0 = ru * ru;
-        T g = c.kc[8];
+        T g = c.kc[11];
 #pragma unroll
-        for (int i = 7; i >= 2; --i) g = fma(g, s0, c.kc[i]);
+        for (int i = 10; i >= 3; --i) g = fma(g, s0, c.kc[i]);
         T t = ru * g;
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
+        const int steps = c.kc[2] > T(1.5) ? 2 : 1;
+#pragma unroll 1
+        for (int it = 0; it < steps; ++it) {
             const T s = t * t;
             const T b3 = fma(k4, s, k3);
             const T c2 = fma(k4, s, b3);
@@ -774,13 +792,15 @@ struct KannalaBrandt {
             t -= f * fma(y0, fma(-fp, y0, T(1)), y0);
         }
         T sn, cs;
+#ifdef ACM_AB_RAY_SINCOS_FALLBACK  // A/B build (Makefile lib/libacm_ab.so)
         sincos_0_2(t, &sn, &cs);
+#else
+        sincos_poly_0_2(t, &sn, &cs);  // theta in [0, pi/2): no OCML fallback
+#endif
         const T q = sn * ir;  // sin(theta) / ru
-        const T px = mx * q, py = my * q;
-        const T in = rsq_nr(fma(px, px, fma(py, py, cs * cs)));
-        X = px * in;
-        Y = py * in;
-        Z = cs * in;
+        X = mx * q;
+        Y = my * q;
+        Z = cs;
     }
 
     // kannala_brandt.rs:445-562: Newton on theta_d(theta) = ru, <=10 steps.

