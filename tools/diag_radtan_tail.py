@@ -21,6 +21,8 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--points", type=int, default=6_250_000)
+    ap.add_argument("--offset", type=int, default=3,
+                    help="synthetic shard (rank) index: points seeded at offset * points")
     a = ap.parse_args()
     import torch
     from apex_camera_models import _lib, samples
@@ -29,7 +31,7 @@ def main():
     params, (w, h) = samples.SAMPLES[1]
     m = MODEL_CLASSES["rad_tan"]._from_params(list(params), Resolution(w, h))
     n = a.points
-    pts = samples.synthetic_points_device(n, offset=3 * n)
+    pts = samples.synthetic_points_device(n, offset=a.offset * n)
     uv, st, _ = m.project_batch(pts)
     cam = m.acm_camera()
     sh = torch.cuda.current_stream().cuda_stream
@@ -68,7 +70,8 @@ def main():
     waves = bad[: (n // 128) * 128].reshape(-1, 128).any(1).float().mean().item()
     gb = 41 * n / 1e9
     print(json.dumps({
-        "what": "RadTan unproject on config-4 pixels", "points": n,
+        "what": "RadTan unproject on config-4 pixels", "points": n, "shard": a.offset,
+        "nonconverging_pixels": int(bad.sum()),
         "nan_fraction": float((~fin).float().mean()),
         "nonconverging_fraction_of_finite": float(bad.float().mean()),
         "waves128_with_nonconverging": waves,
