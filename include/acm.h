@@ -455,6 +455,10 @@ ACM_API int acm_stream_synchronize(void *stream);
  * and their order (-1 = auto = 16 interleaved across the workgroup's four
  * waves, 4 for UCM / EUCM / FOV; 1 = 64 contiguous, 2 = 16 interleaved, 3 = 4 interleaved, 4 = 16
  * contiguous, 5 = 16 interleaved with non-temporal stores).  Same outputs.
+ * ACM_TUNE_NE_SPLIT: Kannala-Brandt normal equations with the sums split
+ * across the waves of a workgroup through LDS (0 = every lane holds all 37
+ * sums, 1 = split, 2 = split capped at 128 VGPRs, -1 = auto).  Same sums up
+ * to summation order.
  * ACM_TUNE_UNPROJECT_RCP: unprojections (acm_unproject, acm_sample_points*)
  * divide by fx, fy through the host's correctly rounded 1/fx, 1/fy and one
  * FMA correction, bit-identical to the division (-1 = auto = on, 0 = plain
@@ -490,7 +494,8 @@ enum {
     ACM_TUNE_NEWTON_FAST = 12,
     ACM_TUNE_UNPROJECT_PPT = 13,
     ACM_TUNE_SAMPLE_CERT = 14,
-    ACM_TUNE_SAMPLE_WRITE = 15
+    ACM_TUNE_SAMPLE_WRITE = 15,
+    ACM_TUNE_NE_SPLIT = 16
 };
 ACM_API int acm_set_tuning(int key, int value);
 
