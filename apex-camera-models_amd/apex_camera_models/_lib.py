@@ -73,7 +73,6 @@ TUNE_NEWTON_FAST = 12  # removed in round 3: acm_set_tuning rejects it (use REFE
 TUNE_UNPROJECT_PPT = 13
 TUNE_SAMPLE_CERT = 14
 TUNE_SAMPLE_WRITE = 15
-TUNE_NE_SPLIT = 16
 ERR_NOT_SUPPORTED = -6
 ERR_NUMERICAL = -7
 LM_TERMINATION = {0: "MaxIterations", 1: "CostTolerance", 2: "ParameterTolerance",

@@ -243,10 +243,6 @@ static std::atomic<int> g_residual_nt{0};
 // 4) and points per lane step (1, 2, 4); 0 = the per-model default below.
 static std::atomic<int> g_ne_waves{0};
 static std::atomic<int> g_ne_unroll{0};
-// KB normal equations: 0 = the per-lane kernel (k_normal_eq), 1 = the
-// wave-split accumulation (k_ne_kb_split), 2 = the same capped at 128 VGPRs,
-// -1 = auto = 1
-static std::atomic<int> g_ne_split{-1};
 // +J launches: -1 = auto = k_project_al (line-aligned store windows; as fast
 // as k_project for N a multiple of 8 and 30-45% faster otherwise,
 // profiles/r01_diag_align.log), 0 = k_project / k_residual, 1 = k_project_al.
@@ -875,30 +871,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         }
         }
     };
-    if constexpr (U == 3) {
-        // one point per lane step, loads issued two steps ahead (twice the
-        // bytes in flight of U = 1 for 5 more registers of data)
-        double x0 = 0, y0 = 0, z0 = 1, x1 = 0, y1 = 0, z1 = 1;
-        double2 o0 = make_double2(0.0, 0.0), o1 = make_double2(0.0, 0.0);
-        if (i < n) {
-            load_point<LAYOUT, NTL>(pts, n, i, x0, y0, z0);
-            o0 = ld2<NTL>(obs + 2 * i);
+    if constexpr (U >= 3) {
+        // one point per lane step, loads issued A = U - 1 steps ahead (A
+        // times the bytes in flight of U = 1 for 5(A-1) more registers).  The
+        // A slots are unrolled, not rotated through register moves: a move of
+        // a register with a load in flight makes the compiler wait for every
+        // load (vmcnt(0)) at the top of each step, which left one step of
+        // latency hiding whatever A was; with static slots each wait is the
+        // counted vmcnt of the slot's own load.
+        constexpr int A = U - 1;
+        double xs[A], ys[A], zs[A];
+        double2 os[A];
+        // branch-free loads (past the end: point n - 1 again, never
+        // accumulated): with loads under exec branches the compiler cannot
+        // count them and waits vmcnt(0)
+        auto load_slot = [&](int q, size_t iq) {
+            const size_t ic = iq < n ? iq : n - 1;
+            load_point<LAYOUT, NTL>(pts, n, ic, xs[q], ys[q], zs[q]);
+            os[q] = ld2<NTL>(obs + 2 * ic);
+        };
+        if (n) {  // (n = 0: nothing to load, the loop below does not run)
+#pragma unroll
+            for (int q = 0; q < A; ++q) load_slot(q, i + (size_t)q * stride);
         }
-        if (i + stride < n) {
-            load_point<LAYOUT, NTL>(pts, n, i + stride, x1, y1, z1);
-            o1 = ld2<NTL>(obs + 2 * (i + stride));
-        }
-        for (; i < n; i += stride) {
-            const size_t i2 = i + 2 * stride;
-            double x2 = 0, y2 = 0, z2 = 1;
-            double2 o2 = make_double2(0.0, 0.0);
-            if (i2 < n) {
-                load_point<LAYOUT, NTL>(pts, n, i2, x2, y2, z2);
-                o2 = ld2<NTL>(obs + 2 * i2);
+        for (; i < n; i += (size_t)A * stride) {
+#pragma unroll
+            for (int q = 0; q < A; ++q) {
+                const size_t iq = i + (size_t)q * stride;
+                if (iq < n) accumulate(xs[q], ys[q], zs[q], os[q]);
+                load_slot(q, iq + (size_t)A * stride);
             }
-            accumulate(x0, y0, z0, o0);
-            x0 = x1; y0 = y1; z0 = z1; o0 = o1;
-            x1 = x2; y1 = y2; z1 = z2; o1 = o2;
         }
     } else if constexpr (U == 1) {
         double x = 0, y = 0, z = 1;
@@ -988,168 +990,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     } else {
         block_sum_store<K>(acc, parts + (size_t)blockIdx.x * K);
     }
-}
-
-// KB normal equations with the accumulation split across the waves of a
-// workgroup (ACM_TUNE_NE_SPLIT).  k_normal_eq<KB> holds
-// all 37 running sums in every lane (74 VGPRs of accumulators, 181 VGPRs
-// in all: 2 waves per SIMD, latency-bound at VALU busy 0.59).  Here each
-// lane projects one point per 256-point chunk and writes the 8 scalars the
-// sums are built from (KannalaBrandt::project_ne) to LDS; then wave w
-// accumulates only its group of the sums over all 256 points of the chunk
-// (4 points per lane): w0 the 10 plain sums (a^2, a, b^2, b, a r0, b r1, r0,
-// r1, r.r, n), w1 the 8 (a fx x_r, b fy y_r) theta^(2k+3), w2 the 12
-// (fx x_r, fy y_r, fx x_r r0 + fy y_r r1) theta^(2k+3), w3 the 7 moments
-// (fx^2 x_r^2 + fy^2 y_r^2) theta^(6+2m).  Invalid points write zeros (their
-// products vanish) and count in `bad` for the sentinel.  Each wave's sums
-// go out in the NE<8> layout, so k_ne_finish is shared.  The order of every
-// sum is fixed: bit-reproducible run to run.
-constexpr int kNeSplitVals = 10;  // a b fxr fyr t2 t3 r0 r1 ok bad
-// WPE = amdgpu_waves_per_eu: 4 caps the kernel at 128 VGPRs.  Left alone
-// the compiler hoists the atan2 polynomial's 19 coefficients into 38 VGPRs
-// for the whole grid-stride loop (154 VGPRs: 3 waves per SIMD).
-template <int LAYOUT, bool NTL, int WPE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_ne_kb_split(acm_camera cam, size_t n,
-                                                        const double* __restrict__ pts,
-                                                        const double* __restrict__ obs,
-                                                        int policy,
-                                                        double* __restrict__ parts) {
-    using M = KannalaBrandt<double>;
-    using L = NE<8>;
-    constexpr int K = L::K;
-    const Cam<double> c = make_cam<double>(cam);
-    const int t = threadIdx.x, lane = t & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-    __shared__ double sv[kNeSplitVals][kBlock];
-    __shared__ double sout[K];
-    const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
-    double acc[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) acc[k] = 0.0;
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    size_t i = (size_t)blockIdx.x * kBlock + t;
-    const size_t first = (size_t)blockIdx.x * kBlock;
-    double x = 0.0, y = 0.0, z = 1.0;
-    double2 o = make_double2(0.0, 0.0);
-    if (i < n) {
-        load_point<LAYOUT, NTL>(pts, n, i, x, y, z);
-        o = ld2<NTL>(obs + 2 * i);
-    }
-    for (size_t base = first; base < n; base += stride, i += stride) {
-        // phase A: this lane's point -> LDS; the next chunk's loads in flight
-        double a = 0, b = 0, fxr = 0, fyr = 0, t2 = 0, t3 = 0, r0 = 0, r1 = 0, ok = 0, bad = 0;
-        if (i < n) {
-            double u, v;
-            const uint8_t st = M::project_ne(c, x, y, z, u, v, a, b, fxr, fyr, t2, t3);
-            if (st == ST_OK) {
-                r0 = u - o.x;
-                r1 = v - o.y;
-                ok = 1.0;
-            } else {
-                a = b = fxr = fyr = t2 = t3 = 0.0;
-                bad = 1.0;
-            }
-        }
-        const size_t inext = i + stride;
-        if (inext < n) {
-            load_point<LAYOUT, NTL>(pts, n, inext, x, y, z);
-            o = ld2<NTL>(obs + 2 * inext);
-        }
-        sv[0][t] = a; sv[1][t] = b; sv[2][t] = fxr; sv[3][t] = fyr;
-        sv[4][t] = t2; sv[5][t] = t3; sv[6][t] = r0; sv[7][t] = r1;
-        sv[8][t] = ok; sv[9][t] = bad;
-        __syncthreads();
-        // phase B: this wave's group of sums over the chunk's 256 points (the
-        // wave branch outside the point loop: one group's operands live at a
-        // time)
-        if (wid == 0) {
-#pragma unroll 2
-            for (int p = lane; p < kBlock; p += 64) {
-                const double pa = sv[0][p], pb = sv[1][p], p0 = sv[6][p], p1 = sv[7][p];
-                acc[0] = fma(pa, pa, acc[0]);
-                acc[1] += pa;
-                acc[2] = fma(pb, pb, acc[2]);
-                acc[3] += pb;
-                acc[4] = fma(pa, p0, acc[4]);
-                acc[5] = fma(pb, p1, acc[5]);
-                acc[6] += p0;
-                acc[7] += p1;
-                acc[8] = fma(p0, p0, fma(p1, p1, fma(sv[9][p], sent2, acc[8])));
-                acc[9] += sv[8][p];
-            }
-        } else if (wid == 1) {
-#pragma unroll 2
-            for (int p = lane; p < kBlock; p += 64) {
-                const double s2 = sv[4][p];
-                const double afx = sv[0][p] * sv[2][p], bfy = sv[1][p] * sv[3][p];
-                double T = sv[5][p];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    acc[k] = fma(afx, T, acc[k]);
-                    acc[4 + k] = fma(bfy, T, acc[4 + k]);
-                    T *= s2;
-                }
-            }
-        } else if (wid == 2) {
-#pragma unroll 2
-            for (int p = lane; p < kBlock; p += 64) {
-                const double s2 = sv[4][p], fx_ = sv[2][p], fy_ = sv[3][p];
-                const double g = fma(fx_, sv[6][p], fy_ * sv[7][p]);
-                double T = sv[5][p];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    acc[k] = fma(fx_, T, acc[k]);
-                    acc[4 + k] = fma(fy_, T, acc[4 + k]);
-                    acc[8 + k] = fma(g, T, acc[8 + k]);
-                    T *= s2;
-                }
-            }
-        } else {
-#pragma unroll 2
-            for (int p = lane; p < kBlock; p += 64) {
-                const double s2 = sv[4][p], fx_ = sv[2][p], fy_ = sv[3][p], t3_ = sv[5][p];
-                double qm = fma(fx_, fx_, fy_ * fy_) * (t3_ * t3_);
-#pragma unroll
-                for (int m = 0; m < 7; ++m) {
-                    acc[m] += qm;
-                    qm *= s2;
-                }
-            }
-        }
-        __syncthreads();  // the LDS tile is rewritten next chunk
-    }
-    // each wave's sums -> the NE<8> layout in LDS, then one store per sum
-    double r[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) r[k] = wave_sum(acc[k]);
-    if (lane == 0) {
-        if (wid == 0) {
-            sout[0] = r[0]; sout[1] = r[1]; sout[L::B2] = r[2]; sout[L::B1] = r[3];
-            sout[L::G + 0] = r[4]; sout[L::G + 1] = r[5]; sout[L::G + 2] = r[6];
-            sout[L::G + 3] = r[7]; sout[K - 2] = r[8]; sout[K - 1] = r[9];
-        } else if (wid == 1) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                sout[L::A_DU + k] = r[k];
-                sout[L::B_DV + k] = r[4 + k];
-            }
-        } else if (wid == 2) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                sout[L::DU + k] = r[k];
-                sout[L::DV + k] = r[4 + k];
-                sout[L::G + 4 + k] = r[8 + k];
-            }
-        } else {
-            int tt = L::DDB;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int k = j; k < 4; ++k, ++tt) sout[tt] = r[j + k];
-        }
-    }
-    __syncthreads();
-    if (t < K) parts[(size_t)blockIdx.x * K + t] = sout[t];
 }
 
 // Epilogue of k_normal_eq in one launch (it was a column-sum kernel plus a
@@ -3439,33 +3279,19 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
         const int wv0 = g_ne_waves, un0 = g_ne_unroll;
         const int wv = wv0 ? wv0 : Def::W;
         const int un = un0 ? un0 : Def::U;
-        // KB: the wave-split accumulation (ACM_TUNE_NE_SPLIT)
-        if constexpr (std::is_same<TagT, Tag<KannalaBrandt>>::value) if (g_ne_split != 0) {
-            const bool ntl = g_nt_loads != 0;
-            auto launch_split = [&](auto kern) {
-                const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
-                if (nb > cap) nb = cap;
-                hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
-                                   points_2d_obs, invalid_policy, parts);
-            };
-            const bool cap4 = g_ne_split == 2;
-            if (layout == ACM_LAYOUT_AOS) {
-                if (cap4) launch_split(ntl ? k_ne_kb_split<ACM_LAYOUT_AOS, true, 4> : k_ne_kb_split<ACM_LAYOUT_AOS, false, 4>);
-                else launch_split(ntl ? k_ne_kb_split<ACM_LAYOUT_AOS, true, 1> : k_ne_kb_split<ACM_LAYOUT_AOS, false, 1>);
-            } else {
-                if (cap4) launch_split(ntl ? k_ne_kb_split<ACM_LAYOUT_SOA, true, 4> : k_ne_kb_split<ACM_LAYOUT_SOA, false, 4>);
-                else launch_split(ntl ? k_ne_kb_split<ACM_LAYOUT_SOA, true, 1> : k_ne_kb_split<ACM_LAYOUT_SOA, false, 1>);
-            }
-            hipLaunchKernelGGL(k_ne_finish<P>, dim3(1), dim3(kNeFinish), 0, s, parts, nb, result,
-                               flag, seq);
-            return check_launch("acm_normal_equations");
-        }
         auto go = [&](auto lay_c, auto w_c) {
             constexpr int LAY = decltype(lay_c)::value, W = decltype(w_c)::value;
             const bool ntl = g_nt_loads != 0;
             auto kern = ntl ? k_normal_eq<TagT, LAY, W, 1, true> : k_normal_eq<TagT, LAY, W, 1, false>;
             if (un == 2) kern = ntl ? k_normal_eq<TagT, LAY, W, 2, true> : k_normal_eq<TagT, LAY, W, 2, false>;
             if (un == 3) kern = ntl ? k_normal_eq<TagT, LAY, W, 3, true> : k_normal_eq<TagT, LAY, W, 3, false>;
+            // 4, 5: loads 3, 4 steps ahead (KB only; others take 3)
+            if constexpr (std::is_same<TagT, Tag<KannalaBrandt>>::value) {
+                if (un == 4) kern = ntl ? k_normal_eq<TagT, LAY, W, 4, true> : k_normal_eq<TagT, LAY, W, 4, false>;
+                if (un == 5) kern = ntl ? k_normal_eq<TagT, LAY, W, 5, true> : k_normal_eq<TagT, LAY, W, 5, false>;
+            } else {
+                if (un >= 4) kern = ntl ? k_normal_eq<TagT, LAY, W, 3, true> : k_normal_eq<TagT, LAY, W, 3, false>;
+            }
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
@@ -4052,7 +3878,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_RESIDUAL_NT, &g_residual_nt, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NE_WAVES, &g_ne_waves, 0, 4, "value must be 0 (per-model default), 1, 3 or 4"},
         {ACM_TUNE_FOV_UNROLL, &g_fov_unroll, 1, 4, "value must be 1, 2 or 4"},
-        {ACM_TUNE_NE_UNROLL, &g_ne_unroll, 0, 3, "value must be 0 (per-model default), 1, 2 or 3"},
+        {ACM_TUNE_NE_UNROLL, &g_ne_unroll, 0, 5, "value must be 0 (per-model default) or 1..5"},
         {ACM_TUNE_ALIGN_J, &g_align_j, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NT_LOADS, &g_nt_loads, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NT_LOADS_UNPROJECT, &g_nt_loads_unproject, -1, 1, "value must be -1..1"},
@@ -4062,7 +3888,6 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_SAMPLE_PATIENCE, &g_sample_patience, -1, 1 << 20, "value must be -1..2^20"},
         {ACM_TUNE_SAMPLE_CERT, &g_sample_cert, -1, 0, "value must be -1 (auto) or 0"},
         {ACM_TUNE_SAMPLE_WRITE, &g_sample_write, -1, 5, "value must be -1..5"},
-        {ACM_TUNE_NE_SPLIT, &g_ne_split, -1, 2, "value must be -1..2"},
         {ACM_TUNE_UNPROJECT_PPT, &g_unproject_ppt, -1, 3, "value must be -1..3"},
     };
     if (key == ACM_TUNE_NEWTON_FAST)  // removed (r03): numerics are chosen per call

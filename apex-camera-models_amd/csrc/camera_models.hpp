@@ -16,7 +16,7 @@
 //     v_rsq_f64 / v_rcp_f64 + two Newton steps (~1 ulp; rsq_nr, rcp_nr) for
 //     r^2, z in [2^-1000, 2^1000] (the IEEE forms outside; ACM_IEEE_MATH
 //     builds the IEEE forms everywhere).  The axis test r < EPS stays exact:
-//     only r^2 < 1e-30 can pass it and that case takes the IEEE sqrt.
+//     it is r^2 < 2^-104 (kAxisR2).
 //   * KB unproject: sin / cos of the Newton angle are polynomials on [0, 2]
 //     (sincos_0_2, OCML beyond), and after the Newton loop 1/ru and 1/|p|
 //     come from rcp_nr / rsq_nr (the IEEE forms outside [2^-1000, 2^1000]).
@@ -85,6 +85,11 @@ constexpr double kPi = 3.141592653589793;
 // for NaN).  Lets the RadTan Newton loop drop two sqrt per step with the
 // reference's decisions unchanged bit for bit (tests/test_capi.py pins it).
 constexpr double kNewtonTol2 = 0x1.19799812dea10p-40;
+// The same for KB's axis test `r < EPS` with r = sqrt(r2) (kannala_brandt.rs
+// :375): 2^-104 = EPS^2 is the smallest double whose correctly rounded sqrt
+// is >= EPS, so `sqrt(r2) < EPS` == `r2 < 2^-104` for every r2 >= 0 and NaN
+// -- no sqrt (the compiler had been computing one for every point).
+constexpr double kAxisR2 = 0x1p-104;
 
 // atan(b) for 0 <= b <= 1: b * P(b^2), P the degree-20 Chebyshev
 // interpolant of atan(sqrt(s))/sqrt(s) on s in [0, 1] (60-digit mpmath fit,
@@ -584,8 +589,7 @@ struct KannalaBrandt {
         if constexpr (sizeof(T) == 8 && !EXACT) {
             // r, 1/r and the atan2 quotient from rsq / rcp + Newton (~1 ulp;
             // the model is already held to 1e-10, not bit-exactness).  The
-            // axis test r < EPS (:375) stays exact: only r2 < 1e-30 can pass
-            // it, and that rare case takes the IEEE sqrt.
+            // axis test r < EPS (:375) stays exact (kAxisR2).
             if (nr_range(r2) && nr_range(z) && z < T(INFINITY)) {
                 ir = rsq_nr(r2);
                 r = r2 * ir;
@@ -598,8 +602,7 @@ struct KannalaBrandt {
                 theta = atan2_ge0(r, z);  // :365 (r >= 0)
                 ir = T(1) / r;
             }
-            axis = false;
-            if (r2 < T(1e-30)) axis = sqrt(r2) < T(kEps);
+            axis = r2 < T(kAxisR2);  // == sqrt(r2) < EPS (:375), exactly
         } else
 #endif
         {
@@ -663,8 +666,7 @@ struct KannalaBrandt {
             theta = atan2_ge0(r, z);
             ir = T(1) / r;
         }
-        axis = false;
-        if (r2 < T(1e-30)) axis = sqrt(r2) < T(kEps);
+        axis = r2 < T(kAxisR2);
 #else
         r = sqrt(r2);
         theta = atan2_ge0(r, z);

@@ -428,8 +428,9 @@ ACM_API int acm_stream_synchronize(void *stream);
  * minimum waves per SIMD the normal-equations kernel is compiled for
  * (0 = per-model default, 1, 3, 4).  ACM_TUNE_FOV_UNROLL: points per lane step of the FOV
  * grid search (1 = default, 2, 4).  ACM_TUNE_NE_UNROLL: points per lane step
- * of the normal-equations kernel (0 = per-model default, 1, 2; 3 = one point
- * per step with its loads issued two steps ahead).
+ * of the normal-equations kernel (0 = per-model default, 1, 2; 3, 4, 5 = one
+ * point per step with its loads issued 2, 3, 4 steps ahead; 4 and 5 are
+ * Kannala-Brandt only, other models take 3).
  * ACM_TUNE_ALIGN_J: kernel of +Jacobian launches of acm_project /
  * acm_residual_jacobian: -1 = auto (default) = line-aligned store windows
  * through LDS, 0 = one point per lane with direct stores, 1 = aligned.
@@ -455,10 +456,6 @@ ACM_API int acm_stream_synchronize(void *stream);
  * and their order (-1 = auto = 16 interleaved across the workgroup's four
  * waves, 4 for UCM / EUCM / FOV; 1 = 64 contiguous, 2 = 16 interleaved, 3 = 4 interleaved, 4 = 16
  * contiguous, 5 = 16 interleaved with non-temporal stores).  Same outputs.
- * ACM_TUNE_NE_SPLIT: Kannala-Brandt normal equations with the sums split
- * across the waves of a workgroup through LDS (0 = every lane holds all 37
- * sums, 1 = split, 2 = split capped at 128 VGPRs, -1 = auto).  Same sums up
- * to summation order.
  * ACM_TUNE_UNPROJECT_RCP: unprojections (acm_unproject, acm_sample_points*)
  * divide by fx, fy through the host's correctly rounded 1/fx, 1/fy and one
  * FMA correction, bit-identical to the division (-1 = auto = on, 0 = plain
@@ -494,8 +491,7 @@ enum {
     ACM_TUNE_NEWTON_FAST = 12,
     ACM_TUNE_UNPROJECT_PPT = 13,
     ACM_TUNE_SAMPLE_CERT = 14,
-    ACM_TUNE_SAMPLE_WRITE = 15,
-    ACM_TUNE_NE_SPLIT = 16
+    ACM_TUNE_SAMPLE_WRITE = 15
 };
 ACM_API int acm_set_tuning(int key, int value);
 

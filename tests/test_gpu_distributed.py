@@ -91,8 +91,10 @@ def test_sharded_gpu_path_matches_single_process(world, tmp_path):
         assert fe[2] == ref.final_reprojection_error.n_valid
         # the sharded sums round differently (~1e-16 relative); RadTan fitted
         # to this 180-degree fisheye is ill-conditioned (half the points fail
-        # to project, mean error 34 px) and amplifies that to ~4e-6 in the
-        # mean, so the check is 1e-5 relative
+        # to project, mean error 34 px): parameters that agree to 1e-8 (the
+        # check above) move the mean error by 4e-6 .. 1.3e-5 relative (runs
+        # r03, r03h), so its check is 1e-4; the other targets 1e-5
+        tol = 1e-4 if tgt == "rad_tan" else 1e-5
         assert abs(fe[0] - ref.final_reprojection_error.mean) <= \
-            1e-5 * ref.final_reprojection_error.mean + 1e-12
+            tol * ref.final_reprojection_error.mean + 1e-12
     torch.cuda.synchronize()

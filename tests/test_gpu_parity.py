@@ -226,26 +226,17 @@ def test_normal_equations_vs_oracle(golden_dir, model, policy):
         torch.as_tensor(xyz), torch.as_tensor(obs), Resolution(w, h), invalid_policy=policy)
     P = len(params)
     A0, b0, c0, nv0 = O.normal_equations(model, params, w, h, xyz, obs, policy)
-    from apex_camera_models import _lib
-    L = _lib.load()
-    # KB: the per-lane kernel (split 0) and the wave-split kernel (1, 2)
-    splits = (0, 1, 2) if model == 2 else (-1,)
-    try:
-        for sp in splits:
-            L.acm_set_tuning(_lib.TUNE_NE_SPLIT, sp)
-            res = f.normal_equations(params)
-            A, b, c, nv = [t.cpu().numpy() for t in f.unpack_normal_equations(res, P)]
-            assert int(nv) == nv0, sp
-            # reduction order differs from the oracle's point order: hold the
-            # sums to 1e-10 of the largest entry (f64 summation of ~2.5k terms)
-            assert np.abs(A - A0).max() <= TOL * np.abs(A0).max(), sp
-            assert np.abs(b - b0).max() <= TOL * max(np.abs(b0).max(), 1.0), sp
-            assert abs(c - c0) <= TOL * max(abs(c0), 1.0), sp
-            # deterministic: a second evaluation is bit-identical
-            res2 = f.normal_equations(params)
-            assert torch.equal(res, res2), sp
-    finally:
-        L.acm_set_tuning(_lib.TUNE_NE_SPLIT, -1)
+    res = f.normal_equations(params)
+    A, b, c, nv = [t.cpu().numpy() for t in f.unpack_normal_equations(res, P)]
+    assert int(nv) == nv0
+    # reduction order differs from the oracle's point order: hold the sums to
+    # 1e-10 of the largest entry (f64 summation of ~2.5k terms)
+    assert np.abs(A - A0).max() <= TOL * np.abs(A0).max()
+    assert np.abs(b - b0).max() <= TOL * max(np.abs(b0).max(), 1.0)
+    assert abs(c - c0) <= TOL * max(abs(c0), 1.0)
+    # deterministic: a second evaluation is bit-identical
+    res2 = f.normal_equations(params)
+    assert torch.equal(res, res2)
 
 
 @pytest.mark.parametrize("model", range(7))
@@ -267,19 +258,16 @@ def test_normal_equations_every_tuning_cell(model):
         torch.as_tensor(xyz), torch.as_tensor(obs), Resolution(w, h))
     P = len(params)
     L = _lib.load()
-    # KB: the (waves, unroll) cells select k_normal_eq under split 0; splits
-    # 1 and 2 are the wave-split kernel (waves / unroll ignored)
-    cells = [(wv, un, ntl, 0 if model == 2 else -1)
-             for wv in (0, 1, 3, 4) for un in (0, 1, 2, 3) for ntl in (-1, 0)]
+    # (KB also: loads 3 and 4 steps ahead)
+    cells = [(wv, un, ntl) for wv in (0, 1, 3, 4) for un in (0, 1, 2, 3) for ntl in (-1, 0)]
     if model == 2:
-        cells += [(0, 0, ntl, sp) for sp in (1, 2) for ntl in (-1, 0)]
+        cells += [(wv, un, -1) for wv in (1, 3) for un in (4, 5)]
     try:
         for cell in cells:
-            wv, un, ntl, sp = cell
+            wv, un, ntl = cell
             L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)
             L.acm_set_tuning(_lib.TUNE_NE_UNROLL, un)
             L.acm_set_tuning(_lib.TUNE_NT_LOADS, ntl)
-            L.acm_set_tuning(_lib.TUNE_NE_SPLIT, sp)
             res = f.normal_equations(params)
             A, b, c, nv = [t.cpu().numpy() for t in f.unpack_normal_equations(res, P)]
             assert int(nv) == nv0, cell
@@ -290,7 +278,6 @@ def test_normal_equations_every_tuning_cell(model):
         L.acm_set_tuning(_lib.TUNE_NE_WAVES, 0)
         L.acm_set_tuning(_lib.TUNE_NE_UNROLL, 0)
         L.acm_set_tuning(_lib.TUNE_NT_LOADS, -1)
-        L.acm_set_tuning(_lib.TUNE_NE_SPLIT, -1)
 
 
 @pytest.mark.parametrize("model", range(7))

@@ -145,33 +145,29 @@ def config3_ne_all(n):
         res = {}
         # nt loads measured 5-11% faster in every cell (profiles/r01_ne_sweep.log);
         # unroll 3 = one point per step, loads two steps ahead
-        # KB: also the wave-split accumulation (ACM_TUNE_NE_SPLIT 1, 2); the
-        # per-lane cells run with split 0
-        combos = [(0, 0, -1, -1)] + [(wv, un, 1, 0) for wv in (1, 3, 4) for un in (1, 2, 3)]
-        if mid == 2:
-            combos += [(0, 0, 1, 1), (0, 0, 1, 2), (0, 0, 0, 1)]
+        combos = [(0, 0, -1)] + [(wv, un, 1) for wv in (1, 3, 4) for un in (1, 2, 3)]
+        if mid == 2:  # KB: loads 3 and 4 steps ahead too
+            combos += [(wv, un, 1) for wv in (1, 3) for un in (4, 5)]
         for rep in range(2):  # interleaved A/B: register target x lane step x nt loads
-            for wv, un, nl, sp in combos:
+            for wv, un, nl in combos:
                 L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)
                 L.acm_set_tuning(_lib.TUNE_NE_UNROLL, un)
                 L.acm_set_tuning(_lib.TUNE_NT_LOADS, nl)
-                L.acm_set_tuning(_lib.TUNE_NE_SPLIT, sp)
-                res.setdefault((wv, un, nl, sp), []).append(
+                res.setdefault((wv, un, nl), []).append(
                     timed(lambda: f.normal_equations(params, out)))
-                if rep == 0 and (wv, un, nl, sp) == combos[0]:
+                if rep == 0 and (wv, un, nl) == combos[0]:
                     ref = out.clone()
                 elif rep == 0:  # grid size / lane order -> summation order
-                    assert torch.allclose(out, ref, rtol=1e-12, atol=0.0), (wv, un, nl, sp)
+                    assert torch.allclose(out, ref, rtol=1e-12, atol=0.0), (wv, un, nl)
         L.acm_set_tuning(_lib.TUNE_NE_WAVES, 0)
         L.acm_set_tuning(_lib.TUNE_NE_UNROLL, 0)
         L.acm_set_tuning(_lib.TUNE_NT_LOADS, -1)
-        L.acm_set_tuning(_lib.TUNE_NE_SPLIT, -1)
         ms = {k: min(v) for k, v in res.items()}
         best = min(ms, key=ms.get)
         emit({"config": 3, "what": "fused normal equations", "model": fcls.MODEL.__name__,
-              "points": n, "ms_by_waves_unroll_ntl_split": {
-                  f"w{k[0]}u{k[1]}n{k[2]}s{k[3]}": round(v, 4) for k, v in ms.items()},
-              "best": f"w{best[0]}u{best[1]}n{best[2]}s{best[3]}",
+              "points": n, "ms_by_waves_unroll_ntl": {
+                  f"w{k[0]}u{k[1]}n{k[2]}": round(v, 4) for k, v in ms.items()},
+              "best": f"w{best[0]}u{best[1]}n{best[2]}",
               "Mpoints_per_s": round(n / ms[best] / 1e3, 1),
               "GBps": round(40 * n / ms[best] / 1e6, 1)})
 
