@@ -756,41 +756,30 @@ static int cu_count() {
     return cus;
 }
 
-// WAVES: minimum waves per SIMD the register allocator must allow
-// (amdgpu_waves_per_eu).  1 leaves it free (KB lands at 176 VGPRs = 2 waves);
-// 3 fits KB in 168 without spills; 4 forces 128 with scratch spills for KB and
-// RadTan.  Selected per launch by ACM_TUNE_NE_WAVES (results identical).
-template <class TagT, int LAYOUT, int WAVES, int U, bool NTL>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq(acm_camera cam, size_t n,
-                                                      const double* __restrict__ pts,
-                                                      const double* __restrict__ obs, int policy,
-                                                      double* __restrict__ parts) {
+// Per-lane running sums of the fused normal equations (k_normal_eq and
+// k_normal_eq_ring): NE<P>'s layout for every model but KB, whose 37 sums
+// are built from powers of theta (below) and expanded to NE<8> at store().
+// FAST projection (reciprocal instead of per-point divisions) and fused
+// multiply-adds: the sums are held to 1e-10, not to the reference's
+// operation order, and the validity mask stays exact (camera_models.hpp).
+template <class TagT>
+struct NeAccum {
     using M = typename TagT::template type<double>;
-    constexpr int P = M::P;
+    static constexpr int P = M::P;
     using L = NE<P>;
-    constexpr int D = L::D;
-    constexpr int K = L::K;
-    const Cam<double> c = make_cam<double>(cam);
-    // KB: 37 running sums in its own layout (kKbNe below) instead of K = 40
-    // -- and no 2 x 8 Jacobian held per point -- expanded to NE<8> once per
-    // lane at the end
-    constexpr bool kKB = std::is_same<TagT, Tag<KannalaBrandt>>::value;
-    constexpr int KA = kKB ? 37 : K;
+    static constexpr int D = L::D;
+    static constexpr int K = L::K;
+    static constexpr bool kKB = std::is_same<TagT, Tag<KannalaBrandt>>::value;
+    static constexpr int KA = kKB ? 37 : K;
     double acc[KA];
+
+    __device__ __forceinline__ void init() {
 #pragma unroll
-    for (int k = 0; k < KA; ++k) acc[k] = 0.0;
-    const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    // Software pipeline: the next U points' 40 bytes each are in flight while
-    // the current U are projected and accumulated (U points per lane step,
-    // ACM_TUNE_NE_UNROLL).  Not for the largest accumulator sets (KB,
-    // RadTan), where the extra registers cost a wave of occupancy.
-    constexpr bool kPrefetch = K <= 40;
-    // FAST projection (reciprocal instead of per-point divisions) and fused
-    // multiply-adds: the sums are held to 1e-10, not to the reference's
-    // operation order, and the validity mask stays exact (camera_models.hpp).
-    auto accumulate = [&](double px, double py, double pz, double2 po) {
+        for (int k = 0; k < KA; ++k) acc[k] = 0.0;
+    }
+
+    __device__ __forceinline__ void add(const Cam<double>& c, double px, double py, double pz,
+                                        double2 po, double sent2) {
         if constexpr (kKB) {
             // KB sums (37): [0] a^2 [1] a [2] b^2 [3] b, [4+k] a fxr T_k,
             // [8+k] b fyr T_k, [12+k] fxr T_k, [16+k] fyr T_k (T_k =
@@ -832,44 +821,104 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             } else {
                 acc[35] += sent2;
             }
-            return;
         } else {
-        double u, v, ju[P], jv[P];
-        const uint8_t st = M::template project<true, true>(c, px, py, pz, u, v, ju, jv);
-        if (st == ST_OK) {
-            const double r0 = u - po.x, r1 = v - po.y;
-            const double a = ju[0], b = jv[1];
-            acc[0] = fma(a, a, acc[0]);
-            acc[1] += a;
-            acc[L::B2] = fma(b, b, acc[L::B2]);
-            acc[L::B1] += b;
+            double u, v, ju[P], jv[P];
+            const uint8_t st = M::template project<true, true>(c, px, py, pz, u, v, ju, jv);
+            if (st == ST_OK) {
+                const double r0 = u - po.x, r1 = v - po.y;
+                const double a = ju[0], b = jv[1];
+                acc[0] = fma(a, a, acc[0]);
+                acc[1] += a;
+                acc[L::B2] = fma(b, b, acc[L::B2]);
+                acc[L::B1] += b;
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                acc[L::A_DU + k] = fma(a, ju[4 + k], acc[L::A_DU + k]);
-                acc[L::B_DV + k] = fma(b, jv[4 + k], acc[L::B_DV + k]);
-                acc[L::DU + k] += ju[4 + k];
-                acc[L::DV + k] += jv[4 + k];
+                for (int k = 0; k < D; ++k) {
+                    acc[L::A_DU + k] = fma(a, ju[4 + k], acc[L::A_DU + k]);
+                    acc[L::B_DV + k] = fma(b, jv[4 + k], acc[L::B_DV + k]);
+                    acc[L::DU + k] += ju[4 + k];
+                    acc[L::DV + k] += jv[4 + k];
+                }
+                int t = L::DDB;
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+#pragma unroll
+                    for (int k = j; k < D; ++k, ++t)
+                        acc[t] = fma(ju[4 + j], ju[4 + k], fma(jv[4 + j], jv[4 + k], acc[t]));
+                }
+                acc[L::G + 0] = fma(a, r0, acc[L::G + 0]);
+                acc[L::G + 1] = fma(b, r1, acc[L::G + 1]);
+                acc[L::G + 2] += r0;
+                acc[L::G + 3] += r1;
+#pragma unroll
+                for (int k = 0; k < D; ++k)
+                    acc[L::G + 4 + k] = fma(ju[4 + k], r0, fma(jv[4 + k], r1, acc[L::G + 4 + k]));
+                acc[K - 2] = fma(r0, r0, fma(r1, r1, acc[K - 2]));
+                acc[K - 1] += 1.0;
+            } else {
+                acc[K - 2] += sent2;
+            }
+        }
+    }
+
+    // workgroup sum of the lanes' sums -> out[0..K) in NE<P>'s layout
+    __device__ __forceinline__ void store(double* __restrict__ out) const {
+        if constexpr (kKB) {  // expand the 37 KB sums into the NE<8> layout
+            static_assert(K == 40, "NE<8>");
+            double full[K];
+            full[0] = acc[0];
+            full[1] = acc[1];
+            full[L::B2] = acc[2];
+            full[L::B1] = acc[3];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                full[L::A_DU + k] = acc[4 + k];
+                full[L::B_DV + k] = acc[8 + k];
+                full[L::DU + k] = acc[12 + k];
+                full[L::DV + k] = acc[16 + k];
+                full[L::G + 4 + k] = acc[31 + k];
             }
             int t = L::DDB;
 #pragma unroll
-            for (int j = 0; j < D; ++j) {
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int k = j; k < D; ++k, ++t)
-                    acc[t] = fma(ju[4 + j], ju[4 + k], fma(jv[4 + j], jv[4 + k], acc[t]));
-            }
-            acc[L::G + 0] = fma(a, r0, acc[L::G + 0]);
-            acc[L::G + 1] = fma(b, r1, acc[L::G + 1]);
-            acc[L::G + 2] += r0;
-            acc[L::G + 3] += r1;
-#pragma unroll
-            for (int k = 0; k < D; ++k)
-                acc[L::G + 4 + k] = fma(ju[4 + k], r0, fma(jv[4 + k], r1, acc[L::G + 4 + k]));
-            acc[K - 2] = fma(r0, r0, fma(r1, r1, acc[K - 2]));
-            acc[K - 1] += 1.0;
+                for (int k = j; k < 4; ++k, ++t) full[t] = acc[20 + j + k];
+            full[L::G + 0] = acc[27];
+            full[L::G + 1] = acc[28];
+            full[L::G + 2] = acc[29];
+            full[L::G + 3] = acc[30];
+            full[K - 2] = acc[35];
+            full[K - 1] = acc[36];
+            block_sum_store<K>(full, out);
         } else {
-            acc[K - 2] += sent2;
+            block_sum_store<K>(acc, out);
         }
-        }
+    }
+};
+
+// WAVES: minimum waves per SIMD the register allocator must allow
+// (amdgpu_waves_per_eu).  1 leaves it free (KB lands at 176 VGPRs = 2 waves);
+// 3 fits KB in 168 without spills; 4 forces 128 with scratch spills for KB and
+// RadTan.  Selected per launch by ACM_TUNE_NE_WAVES (results identical).
+template <class TagT, int LAYOUT, int WAVES, int U, bool NTL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq(acm_camera cam, size_t n,
+                                                      const double* __restrict__ pts,
+                                                      const double* __restrict__ obs, int policy,
+                                                      double* __restrict__ parts) {
+    using Acc = NeAccum<TagT>;
+    constexpr int K = Acc::K;
+    const Cam<double> c = make_cam<double>(cam);
+    Acc sums;
+    sums.init();
+    const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    // Software pipeline: the next U points' 40 bytes each are in flight while
+    // the current U are projected and accumulated (U points per lane step,
+    // ACM_TUNE_NE_UNROLL).  Not for the largest accumulator sets (KB,
+    // RadTan), where the extra registers cost a wave of occupancy.
+    constexpr bool kPrefetch = K <= 40;
+    auto accumulate = [&](double px, double py, double pz, double2 po) {
+        sums.add(c, px, py, pz, po, sent2);
     };
     if constexpr (U >= 3) {
         // one point per lane step, loads issued A = U - 1 steps ahead (A
@@ -960,36 +1009,129 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             }
         }
     }
-    if constexpr (kKB) {  // expand the 37 KB sums into the NE<8> layout
-        static_assert(K == 40, "NE<8>");
-        double full[K];
-        full[0] = acc[0];
-        full[1] = acc[1];
-        full[L::B2] = acc[2];
-        full[L::B1] = acc[3];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            full[L::A_DU + k] = acc[4 + k];
-            full[L::B_DV + k] = acc[8 + k];
-            full[L::DU + k] = acc[12 + k];
-            full[L::DV + k] = acc[16 + k];
-            full[L::G + 4 + k] = acc[31 + k];
-        }
-        int t = L::DDB;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int k = j; k < 4; ++k, ++t) full[t] = acc[20 + j + k];
-        full[L::G + 0] = acc[27];
-        full[L::G + 1] = acc[28];
-        full[L::G + 2] = acc[29];
-        full[L::G + 3] = acc[30];
-        full[K - 2] = acc[35];
-        full[K - 1] = acc[36];
-        block_sum_store<K>(full, parts + (size_t)blockIdx.x * K);
-    } else {
-        block_sum_store<K>(acc, parts + (size_t)blockIdx.x * K);
+    sums.store(parts + (size_t)blockIdx.x * K);
+}
+
+// k_normal_eq_ring: the same sums with the AoS point and observation streams
+// staged through a per-wave LDS ring by LDS-DMA (global_load_lds: the data
+// lands in LDS, no VGPR destination).  A wave takes 64 consecutive points per
+// step (1536 B of points as 16-B-per-lane pieces from 64 + 32 lanes + 1024 B
+// of observations as one 16-B-per-lane piece, in the bytes' order, so each lane then
+// reads its own point from LDS) and keeps the next S - 1 steps' loads in
+// flight.  (AoS points and observations on a 16-B boundary: the launcher
+// takes k_normal_eq otherwise.)  The register prefetch of k_normal_eq holds 10 VGPRs per step of
+// lookahead and the compiler's conservative vmcnt over its exec branches
+// waited for the next slot's loads mid-step (profiles/r03l_*); here the
+// lookahead costs LDS only and every wait is an explicit counted vmcnt.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+constexpr int kRingSlot = 320;  // doubles per wave slot: 64 x (3 + 2)
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// waves per SIMD a ring of S slots leaves room for in the 160 KB of LDS
+// (one wave per SIMD per workgroup), capping the register target
+template <int W, int S>
+struct RingWaves {
+    static constexpr int lds = 4 * S * kRingSlot * 8 + 2048;
+    static constexpr int fit = (160 * 1024) / lds;
+    static constexpr int value = W < fit ? W : fit;
+};
+
+// s_waitcnt vmcnt(3 * ahead): every load but the `ahead` newest steps' three
+__device__ __forceinline__ void ring_wait(int ahead) {
+    switch (ahead) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
     }
+}
+
+template <class TagT, int WAVES, int S, bool NTL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RingWaves<WAVES, S>::value))) void k_normal_eq_ring(
+        acm_camera cam, size_t n, const double* __restrict__ pts, const double* __restrict__ obs,
+        int policy, double* __restrict__ parts) {
+    static_assert(S >= 2 && S <= 6, "ring depth");
+    using Acc = NeAccum<TagT>;
+    constexpr int K = Acc::K;
+    constexpr int kWaves = kBlock / 64;
+    __shared__ __attribute__((aligned(16))) double ring[kWaves][S][kRingSlot];
+    const Cam<double> c = make_cam<double>(cam);
+    Acc sums;
+    sums.init();
+    const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const size_t nw = (size_t)gridDim.x * kWaves;
+    // the ring takes an even number of points, so its last 16-B piece of
+    // points ends on the last point (24 nr = 16 x 3nr/2); an odd n's last
+    // point is added after the loop by plain loads
+    const size_t nr = n & ~(size_t)1;
+    const size_t nc = (nr + 63) / 64;  // 64-point steps
+    const size_t pbytes = nr * 24, obytes = nr * 16;
+    const char* pb = reinterpret_cast<const char*>(pts);
+    const char* ob = reinterpret_cast<const char*>(obs);
+    constexpr unsigned kAux = NTL ? 2u : 0u;  // nt
+    // one step's three 16-B-per-lane LDS-DMA loads into `slot`: points
+    // bytes [0, 1024) by all lanes and [1024, 1536) by lanes 0-31 (the
+    // others masked off: they neither read nor write), observations by all;
+    // pieces past the end of a stream read its first bytes instead (never
+    // accumulated).  (The 12-B form, global_load_lds_dwordx3, does not place
+    // lane l at base + 12 l on gfx950: measured wrong sums.)
+    auto issue = [&](int slot, size_t step) {
+        double* d = &ring[wid][slot][0];
+        const size_t p0 = step * 1536 + (size_t)lane * 16, p1 = p0 + 1024;
+        const size_t o0 = step * 1024 + (size_t)lane * 16;
+        const char* s0 = pb + (p0 + 16 <= pbytes ? p0 : 0);
+        const char* s1 = pb + (p1 + 16 <= pbytes ? p1 : 0);
+        const char* s2 = ob + (o0 + 16 <= obytes ? o0 : 0);
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)s0, (lds_void_t*)d, 16, 0, kAux);
+        if (lane < 32)
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)s1, (lds_void_t*)(d + 128), 16, 0, kAux);
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)s2, (lds_void_t*)(d + 192), 16, 0, kAux);
+    };
+    size_t step = (size_t)blockIdx.x * kWaves + wid;
+#pragma unroll
+    for (int q = 0; q < S - 1; ++q) {
+        const size_t sq = step + (size_t)q * nw;
+        if (sq < nc) issue(q, sq);
+    }
+    int slot = 0;
+    for (; step < nc; step += nw) {
+        // the slot read one step ago takes the step S - 1 ahead (its LDS
+        // reads were consumed by that step's sums)
+        const size_t sn = step + (size_t)(S - 1) * nw;
+        if (sn < nc) issue(slot == 0 ? S - 1 : slot - 1, sn);
+        const size_t left = (nc - 1 - step) / nw;  // this wave's steps after this one
+        ring_wait(left < (size_t)(S - 1) ? (int)left : S - 1);
+        // the lane's 24 + 16 bytes, read in inline asm: a compiler-visible
+        // LDS read after an LDS-DMA gets a vmcnt(0) from the compiler (it
+        // cannot tell the slots apart), which would drain the ring
+        dbl2 xy, o;
+        double pz;
+        const double* d = &ring[wid][slot][0];
+        asm volatile(
+                "ds_read2_b64 %0, %3 offset1:1\n\t"
+                "ds_read_b64 %1, %3 offset:16\n\t"
+                "ds_read_b128 %2, %4\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=v"(xy), "=v"(pz), "=v"(o)
+                : "v"(lds_addr(d + 3 * lane)), "v"(lds_addr(d + 192 + 2 * lane))
+                : "memory");
+        if (step * 64 + lane < nr) sums.add(c, xy.x, xy.y, pz, make_double2(o.x, o.y), sent2);
+        slot = slot + 1 == S ? 0 : slot + 1;
+    }
+    if (nr != n && blockIdx.x == 0 && threadIdx.x == 0) {  // (no LDS-DMA in flight)
+        double x, y, z;
+        load_point<ACM_LAYOUT_AOS>(pts, n, n - 1, x, y, z);
+        sums.add(c, x, y, z, ld2<false>(obs + 2 * (n - 1)), sent2);
+    }
+    sums.store(parts + (size_t)blockIdx.x * K);
 }
 
 // Epilogue of k_normal_eq in one launch (it was a column-sum kernel plus a
@@ -1737,13 +1879,25 @@ __global__ __launch_bounds__(kBlock) void k_seg_count(CamArg cam, Grid g, size_t
 // ballot their rank, each writes its 16-B pixel at offset + rank, and the
 // compacted rays (3 * kept doubles, staged in the wave's 1.5 KiB of LDS) go
 // out as 16-B pieces.  A segment whose count is 0 is skipped.
-template <class TagT, int SPW, bool ILV, bool NT = false>
+//
+// FIX (the repair pass of the speculative path, k_seg_spec): the segments
+// were already written at their speculative offsets (64 x segment); rewrite
+// only those whose true offset differs and that keep something -- none at
+// all when nothing was dropped (total == cells).
+template <class TagT, int SPW, bool ILV, bool NT = false, bool FIX = false>
 __global__ __launch_bounds__(kBlock) void k_seg_write(CamArg cam, Grid g, size_t cells,
                                                       const uint32_t* __restrict__ seg_cnt,
                                                       const uint64_t* __restrict__ blk_off,
                                                       double* __restrict__ uv_out,
-                                                      double* __restrict__ xyz_out) {
+                                                      double* __restrict__ xyz_out,
+                                                      const uint64_t* __restrict__ total) {
     static_assert(kSegPerBlock % (4 * SPW) == 0, "write workgroups tile the count blocks");
+    if constexpr (FIX) {
+        if (total[0] == (uint64_t)cells) return;  // every cell kept: all in place
+        // segments before this workgroup's count block all full: its
+        // segments' speculative offsets are right up to its first partial one
+        // -- the scan below decides per segment
+    }
     const Cam<double> c = make_cam<double>(cam);
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1787,6 +1941,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(CamArg cam, Grid g, size_t
         const uint32_t sc = __builtin_amdgcn_readfirstlane(s_cnt[li]);
         if (sc == 0) continue;  // nothing kept here (certified or counted)
         const uint64_t off = uniform64(s_off[li]);
+        if (FIX && off == sg * kSegCells) continue;  // already in place
         const uint64_t cell = sg * kSegCells + lane;
         double u = 0.0, v = 0.0, X = 0.0, Y = 0.0, Z = 0.0;
         bool keep = false;
@@ -1819,6 +1974,91 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(CamArg cam, Grid g, size_t
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+// Speculative segment path (ACM_TUNE_SAMPLE_FUSED = 4; auto for RadTan,
+// which has no keep certificate, so a count pass would run its Newton loop
+// for every cell).  One pass unprojects every segment once and writes its
+// kept points compacted within the segment's own speculative range [64 s,
+// 64 s + count) -- the final place whenever no cell before it was dropped
+// (the output buffers hold every cell of the range, acm.h) -- and records
+// the per-segment and per-count-block counts.  k_scan_counts then gives the
+// true offsets and the total, and k_seg_write<FIX> recomputes and rewrites
+// only the segments whose true offset differs.  Grids that keep every cell
+// (RadTan's sample camera) cost one unprojection pass plus two tiny
+// launches; a grid whose first drop comes early pays the write pass again
+// over the segments after it.  Outputs are bit-identical to every other
+// path (the same per-cell function, the same order).
+template <class TagT>
+__global__ __launch_bounds__(kBlock) void k_seg_spec(CamArg cam, Grid g, size_t cells,
+                                                     uint32_t* __restrict__ seg_cnt,
+                                                     uint64_t* __restrict__ blk_sum,
+                                                     double* __restrict__ uv_out,
+                                                     double* __restrict__ xyz_out) {
+    // one workgroup per count block (256 segments), wave w takes segments
+    // w, w + 4, ... so the four waves write adjacent runs at the same time
+    constexpr int SPW = kSegPerBlock / 4;
+    const Cam<double> c = make_cam<double>(cam);
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nseg = (cells + kSegCells - 1) / kSegCells;
+    const uint64_t seg0 = (uint64_t)blockIdx.x * kSegPerBlock;
+    __shared__ double s_ray[kBlock / 64][64 * 3];
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    const uint64_t below = lane ? ((~0ull) >> (64 - lane)) : 0ull;
+    double* lx = s_ray[wid];
+    constexpr uint32_t kStep = 4 * kSegCells;
+    CellWalk cw;
+    cw.init(g, (seg0 + (uint64_t)wid) * kSegCells, lane);
+    uint32_t wsum = 0;
+#pragma unroll 1
+    for (int k = 0; k < SPW; ++k, cw.template step_by<kStep>(g)) {
+        const uint64_t sg = seg0 + (uint64_t)(wid + 4 * k);
+        if (sg >= nseg) break;
+        const uint64_t cell = sg * kSegCells + lane;
+        double u = 0.0, v = 0.0, X = 0.0, Y = 0.0, Z = 0.0;
+        bool keep = false;
+        if (cell < cells) keep = sample_cell<TagT>(c, g, cw, u, v, X, Y, Z);
+        const uint64_t m = __ballot(keep);
+        const uint32_t kc = (uint32_t)__popcll(m);
+        if (lane == 0) seg_cnt[sg] = kc;
+        wsum += kc;
+        if (kc == 0) continue;
+        const uint64_t off = sg * kSegCells;
+        const uint32_t rank = (uint32_t)__popcll(m & below);
+        if (keep) {
+            st2<false>(uv_out + 2 * (off + rank), u, v);
+            double* d = lx + 3 * rank;
+            d[0] = X;
+            d[1] = Y;
+            d[2] = Z;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // 3 * 64 * sg doubles: the rays start on the 16-B grid when xyz_out
+        // does
+        double* dst = xyz_out + 3 * off;
+        const uint32_t nd = 3 * kc;
+        const uint32_t h = (uint32_t)((reinterpret_cast<uintptr_t>(dst) >> 3) & 1u);
+        const uint32_t np = (nd - h) >> 1;
+        for (uint32_t p = lane; p < np; p += 64) {
+            const uint32_t dd = h + 2 * p;
+            st2<false>(dst + dd, lx[dd], lx[dd + 1]);
+        }
+        if (lane == 0 && h) dst[0] = lx[0];
+        if (lane == 63 && ((nd - h) & 1u)) dst[nd - 1] = lx[nd - 1];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0) s_wsum[wid] = wsum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += s_wsum[w];
+        blk_sum[blockIdx.x] = t;
     }
 }
 
@@ -3292,6 +3532,19 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
             } else {
                 if (un >= 4) kern = ntl ? k_normal_eq<TagT, LAY, W, 3, true> : k_normal_eq<TagT, LAY, W, 3, false>;
             }
+            // 6, 7, 8: the LDS-DMA ring of 3, 4, 6 steps (AoS points; SoA
+            // takes 3)
+            const bool al16 = ((reinterpret_cast<uintptr_t>(points_3d) |
+                                reinterpret_cast<uintptr_t>(points_2d_obs)) & 15u) == 0;
+            if (LAY == ACM_LAYOUT_AOS && !al16 && un >= 6)
+                kern = ntl ? k_normal_eq<TagT, LAY, W, 3, true> : k_normal_eq<TagT, LAY, W, 3, false>;
+            else if constexpr (LAY == ACM_LAYOUT_AOS) {
+                if (un == 6) kern = ntl ? k_normal_eq_ring<TagT, W, 3, true> : k_normal_eq_ring<TagT, W, 3, false>;
+                if (un == 7) kern = ntl ? k_normal_eq_ring<TagT, W, 4, true> : k_normal_eq_ring<TagT, W, 4, false>;
+                if (un == 8) kern = ntl ? k_normal_eq_ring<TagT, W, 6, true> : k_normal_eq_ring<TagT, W, 6, false>;
+            } else if (un >= 6) {
+                kern = ntl ? k_normal_eq<TagT, LAY, W, 3, true> : k_normal_eq<TagT, LAY, W, 3, false>;
+            }
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
@@ -3511,7 +3764,8 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
     // keeps the single pass for it (1.32 vs 1.78 ms at 1e8 cells,
     // profiles/r03c_diag_sample.log)
     if (mode < 0 && cam->model == ACM_RADTAN) mode = 2;
-    if (mode < 0) {  // segment two-pass (default)
+    const bool spec = mode == 4;
+    if (mode < 0 || spec) {  // segment two-pass (default) / speculative segments
         const size_t nseg = (cells + kSegCells - 1) / kSegCells;
         const size_t nsb = (cells + kSegBlockCells - 1) / kSegBlockCells;
         uint32_t* seg_cnt = (uint32_t*)workspace;
@@ -3520,10 +3774,6 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
         const SegCert cert = seg_cert(*cam);
         return dispatch_model(cam->model, [&](auto tag) -> int {
             using TagT = decltype(tag);
-            hipLaunchKernelGGL((k_seg_count<TagT>), dim3((unsigned)nsb), dim3(kBlock), 0, s, ca, g,
-                               cells, cert, seg_cnt, blk_sum);
-            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, blk_sum, nsb, blk_off,
-                               counts, (uint64_t)cells);
             // ACM_TUNE_SAMPLE_WRITE: segments per write wave and order
             // (-1 auto = 16 interleaved; 1 = 64 contiguous, 2 = 16
             // interleaved, 3 = 4 interleaved, 4 = 16 contiguous, 5 = 16
@@ -3538,8 +3788,21 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
             auto wlaunch = [&](auto kern, int spw) {
                 const size_t nwb = (nseg + 4 * (size_t)spw - 1) / (4 * (size_t)spw);
                 hipLaunchKernelGGL(kern, dim3((unsigned)nwb), dim3(kBlock), 0, s, ca, g, cells,
-                                   seg_cnt, blk_off, points_2d_out, points_3d_out);
+                                   seg_cnt, blk_off, points_2d_out, points_3d_out,
+                                   (const uint64_t*)counts);
             };
+            if (spec) {
+                hipLaunchKernelGGL((k_seg_spec<TagT>), dim3((unsigned)nsb), dim3(kBlock), 0, s, ca,
+                                   g, cells, seg_cnt, blk_sum, points_2d_out, points_3d_out);
+                hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, blk_sum, nsb, blk_off,
+                                   counts, (uint64_t)cells);
+                wlaunch(k_seg_write<TagT, 16, true, false, true>, 16);
+                return check_launch("acm_sample_points");
+            }
+            hipLaunchKernelGGL((k_seg_count<TagT>), dim3((unsigned)nsb), dim3(kBlock), 0, s, ca, g,
+                               cells, cert, seg_cnt, blk_sum);
+            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, blk_sum, nsb, blk_off,
+                               counts, (uint64_t)cells);
             if (wv == 5) wlaunch(k_seg_write<TagT, 16, true, true>, 16);
             else if (wv == 1) wlaunch(k_seg_write<TagT, 64, false>, 64);
             else if (wv == 3) wlaunch(k_seg_write<TagT, 4, true>, 4);
@@ -3878,12 +4141,12 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_RESIDUAL_NT, &g_residual_nt, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NE_WAVES, &g_ne_waves, 0, 4, "value must be 0 (per-model default), 1, 3 or 4"},
         {ACM_TUNE_FOV_UNROLL, &g_fov_unroll, 1, 4, "value must be 1, 2 or 4"},
-        {ACM_TUNE_NE_UNROLL, &g_ne_unroll, 0, 5, "value must be 0 (per-model default) or 1..5"},
+        {ACM_TUNE_NE_UNROLL, &g_ne_unroll, 0, 8, "value must be 0 (per-model default) or 1..8"},
         {ACM_TUNE_ALIGN_J, &g_align_j, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NT_LOADS, &g_nt_loads, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NT_LOADS_UNPROJECT, &g_nt_loads_unproject, -1, 1, "value must be -1..1"},
         {ACM_TUNE_LM_HOST_RESULT, &g_lm_host_result, -1, 2, "value must be -1..2"},
-        {ACM_TUNE_SAMPLE_FUSED, &g_sample_fused, -1, 3, "value must be -1..3"},
+        {ACM_TUNE_SAMPLE_FUSED, &g_sample_fused, -1, 4, "value must be -1..4"},
         {ACM_TUNE_UNPROJECT_RCP, &g_unproject_rcp, -1, 1, "value must be -1..1"},
         {ACM_TUNE_SAMPLE_PATIENCE, &g_sample_patience, -1, 1 << 20, "value must be -1..2^20"},
         {ACM_TUNE_SAMPLE_CERT, &g_sample_cert, -1, 0, "value must be -1 (auto) or 0"},

@@ -430,7 +430,9 @@ ACM_API int acm_stream_synchronize(void *stream);
  * grid search (1 = default, 2, 4).  ACM_TUNE_NE_UNROLL: points per lane step
  * of the normal-equations kernel (0 = per-model default, 1, 2; 3, 4, 5 = one
  * point per step with its loads issued 2, 3, 4 steps ahead; 4 and 5 are
- * Kannala-Brandt only, other models take 3).
+ * Kannala-Brandt only, other models take 3; 6, 7, 8 = the LDS-DMA ring of
+ * 3, 4, 6 steps of 64 points per wave, for AoS points and observations on a
+ * 16-B boundary, 3 otherwise).
  * ACM_TUNE_ALIGN_J: kernel of +Jacobian launches of acm_project /
  * acm_residual_jacobian: -1 = auto (default) = line-aligned store windows
  * through LDS, 0 = one point per lane with direct stores, 1 = aligned.
@@ -448,7 +450,10 @@ ACM_API int acm_stream_synchronize(void *stream);
  * then a write pass with known offsets); 0 = the round-1 two-pass count /
  * scan / recompute-and-write path (tiles of 16 x 256 cells); 1 / 2 / 3 = the
  * single pass with a decoupled look-back, tiles of 2 / 4 / 8 x 256 cells
- * (round 1 mapped 1 / 2 / 3 to 4 / 8 / 16 x 256; changed in round 2).
+ * (round 1 mapped 1 / 2 / 3 to 4 / 8 / 16 x 256; changed in round 2); 4 =
+ * speculative segments (r03): one pass writes every segment of 64 cells in
+ * place as if nothing before it was dropped, a scan gives the true offsets
+ * and a repair pass rewrites only the segments after the first drop.
  * Outputs are identical for every value.
  * ACM_TUNE_SAMPLE_CERT: the segment path's host-certified keep regions
  * (-1 = auto = on; 0 = every segment counted cell by cell).  Same outputs.

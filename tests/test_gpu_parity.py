@@ -262,6 +262,8 @@ def test_normal_equations_every_tuning_cell(model):
     cells = [(wv, un, ntl) for wv in (0, 1, 3, 4) for un in (0, 1, 2, 3) for ntl in (-1, 0)]
     if model == 2:
         cells += [(wv, un, -1) for wv in (1, 3) for un in (4, 5)]
+    # the LDS-DMA ring of 3 / 4 / 6 steps (k_normal_eq_ring)
+    cells += [(wv, un, ntl) for wv in (1, 3, 4) for un in (6, 7, 8) for ntl in (-1, 0)]
     try:
         for cell in cells:
             wv, un, ntl = cell
@@ -278,6 +280,50 @@ def test_normal_equations_every_tuning_cell(model):
         L.acm_set_tuning(_lib.TUNE_NE_WAVES, 0)
         L.acm_set_tuning(_lib.TUNE_NE_UNROLL, 0)
         L.acm_set_tuning(_lib.TUNE_NT_LOADS, -1)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 64 * 3 * 2048 + 17])
+@pytest.mark.parametrize("policy", [0, 1])
+def test_normal_equations_ring_ragged(n, policy):
+    """k_normal_eq_ring on batches shorter than one wave step, one step plus
+    one point, and just past a whole number of ring rounds: every wave's
+    tail (fewer steps than the ring depth, none at all) matches the oracle."""
+    import torch
+    from apex_camera_models import _lib, factors, samples
+    from apex_camera_models.camera import Resolution
+    L = _lib.load()
+    for model in (2, 3):
+        params, (w, h) = samples.SAMPLES[model]
+        xyz = samples.synthetic_points(n + 64)[:n]
+        xyz = np.where(np.isfinite(xyz), xyz, 1.0)
+        uv0, _, _ = O.project(model, params, w, h, xyz)
+        obs = np.where(np.isnan(uv0), 3.0, uv0) + 0.25
+        A0, b0, c0, nv0 = O.normal_equations(model, params, w, h, xyz, obs, policy)
+        f = factors.CameraParamsFactor.__subclasses__()[model](
+            torch.as_tensor(xyz), torch.as_tensor(obs), Resolution(w, h), invalid_policy=policy)
+        P = len(params)
+        try:
+            for un in (6, 7, 8):
+                L.acm_set_tuning(_lib.TUNE_NE_UNROLL, un)
+                res = f.normal_equations(params)
+                A, b, c, nv = [t.cpu().numpy() for t in f.unpack_normal_equations(res, P)]
+                assert int(nv) == nv0, (model, un)
+                assert np.abs(A - A0).max() <= TOL * max(np.abs(A0).max(), 1.0), (model, un)
+                assert np.abs(b - b0).max() <= TOL * max(np.abs(b0).max(), 1.0), (model, un)
+                assert abs(c - c0) <= TOL * max(abs(c0), 1.0), (model, un)
+            # points / observations off the 16-B grid: the launcher falls
+            # back to the register-prefetch kernel (same sums)
+            xb = torch.as_tensor(np.concatenate([xyz[:1], xyz]), device="cuda")[1:]
+            obb = torch.as_tensor(np.concatenate([obs[:1], obs]), device="cuda")[1:]
+            fb = factors.CameraParamsFactor.__subclasses__()[model](
+                xb, obb, Resolution(w, h), invalid_policy=policy)
+            assert fb.points_3d.data_ptr() % 16 == 8
+            L.acm_set_tuning(_lib.TUNE_NE_UNROLL, 7)
+            A, b, c, nv = [t.cpu().numpy() for t in fb.unpack_normal_equations(
+                fb.normal_equations(params), P)]
+            assert int(nv) == nv0 and np.abs(A - A0).max() <= TOL * max(np.abs(A0).max(), 1.0)
+        finally:
+            L.acm_set_tuning(_lib.TUNE_NE_UNROLL, 0)
 
 
 @pytest.mark.parametrize("model", range(7))
@@ -372,7 +418,7 @@ def test_sample_points_every_path_matches_oracle(model):
     ncx = int(round(np.sqrt(n * (w / h))))
     ncy = int(round(np.sqrt(n * (h / w))))
     try:
-        for v in (-1, 0, 1, 2, 3):
+        for v in (-1, 0, 1, 2, 3, 4):
             L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, v)
             uv, xyz = util.sample_points(m, n)
             assert np.array_equal(uv.cpu().numpy(), uv0), v
@@ -405,6 +451,44 @@ def test_sample_points_kb_clamped_angle():
         assert rel_err(xyz.cpu().numpy(), xyz0, floor=1.0) <= TOL
         # the clamped pixels are there (Z tiny but positive)
         assert (xyz0[:, 2] < 1e-15).sum() > 0
+
+
+@pytest.mark.parametrize("case", range(len(NEWTON_STRESS)))
+def test_sample_points_speculative_with_drops(case):
+    """The speculative segment path (ACM_TUNE_SAMPLE_FUSED = 4, auto for
+    RadTan) on the strongly distorted cameras, whose Newton fails over whole
+    regions of the image: the repair pass must move every segment after the
+    first drop, and the result equals the segment two-pass path, the
+    round-1 two-pass path and the oracle bit for bit -- also per row-range
+    shard, whose first drop comes at a different place."""
+    import torch
+    from apex_camera_models import _lib, util
+    from apex_camera_models.distributed import gpu_sample_points_range, grid_row_range
+    model, params, (w, h) = NEWTON_STRESS[case]
+    m = _model_obj(model, params, w, h)
+    n = 400_000
+    L = _lib.load()
+    ncx = int(round(np.sqrt(n * (w / h))))
+    ncy = int(round(np.sqrt(n * (h / w))))
+    try:
+        outs = {}
+        for v in (4, 0, -1):
+            L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, v)
+            outs[v] = util.sample_points(m, n)
+            if v == 4:
+                fn = gpu_sample_points_range(m, n)
+                parts = [fn(*grid_row_range(ncx, ncy, r, 3)) for r in range(3)]
+        uv, xyz = outs[4]
+        for v in (0, -1):
+            assert torch_equal_bits(uv, outs[v][0]) and torch_equal_bits(xyz, outs[v][1]), v
+        assert torch.equal(torch.cat([p[0] for p in parts]), uv)
+        assert torch.equal(torch.cat([p[1] for p in parts]), xyz)
+    finally:
+        L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, -1)
+    assert uv.shape[0] < ncx * ncy  # this camera drops cells
+    uv0, xyz0, _ = O.sample_points(model, params, w, h, n)
+    assert np.array_equal(uv.cpu().numpy(), uv0)
+    assert rel_err(xyz.cpu().numpy(), xyz0, floor=1.0) <= TOL
 
 
 @pytest.mark.parametrize("fused", [1, 2, 3])

@@ -148,6 +148,8 @@ def config3_ne_all(n):
         combos = [(0, 0, -1)] + [(wv, un, 1) for wv in (1, 3, 4) for un in (1, 2, 3)]
         if mid == 2:  # KB: loads 3 and 4 steps ahead too
             combos += [(wv, un, 1) for wv in (1, 3) for un in (4, 5)]
+        # 6 / 7 / 8: the LDS-DMA ring of 3 / 4 / 6 steps (AoS points)
+        combos += [(wv, un, 1) for wv in (1, 3, 4) for un in (6, 7, 8)]
         for rep in range(2):  # interleaved A/B: register target x lane step x nt loads
             for wv, un, nl in combos:
                 L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)

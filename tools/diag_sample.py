@@ -2,7 +2,8 @@
 two-pass default ("seg"; "seg_nocert" = ACM_TUNE_SAMPLE_CERT 0, every
 segment counted cell by cell; "seg_w1".."seg_w4" = ACM_TUNE_SAMPLE_WRITE),
 the round-1 two-pass count / scan / write path ("two_pass") and the single
-pass with a decoupled look-back ("fused_r2" / "_r4" / "_r8"), every
+pass with a decoupled look-back ("fused_r2" / "_r4" / "_r8"), the
+speculative segment path ("spec": write in place, repair after a drop), every
 model on the config-5 grid (1e8 requested cells), interleaved in one
 process.  The outputs must be bit-identical.
 
@@ -36,7 +37,8 @@ def main():
         # variant names: seg (default), seg_nocert, seg_w1..seg_w4
         # (ACM_TUNE_SAMPLE_WRITE), two_pass, fused_r2 / r4 / r8
         def run_knobs(v):
-            fused = {"two_pass": 0, "fused_r2": 1, "fused_r4": 2, "fused_r8": 3}.get(v, -1)
+            fused = {"two_pass": 0, "fused_r2": 1, "fused_r4": 2, "fused_r8": 3,
+                     "spec": 4}.get(v, -1)
             L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, fused)
             L.acm_set_tuning(_lib.TUNE_SAMPLE_CERT, 0 if v == "seg_nocert" else -1)
             L.acm_set_tuning(_lib.TUNE_SAMPLE_WRITE, int(v[-1]) if v.startswith("seg_w") else -1)
