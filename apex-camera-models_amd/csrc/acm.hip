@@ -256,7 +256,7 @@ static std::atomic<int> g_nt_loads{-1};
 // every model (profiles/r01_diag_ntl.log).
 static std::atomic<int> g_nt_loads_unproject{-1};
 // FOV grid search: points per lane step (1 = default, 2, 4).
-static std::atomic<int> g_fov_unroll{1};
+static std::atomic<int> g_fov_unroll{-1};
 // sample_points: -1 = auto = single pass with decoupled look-back and the
 // per-model tile (SampleR), 0 = the two-pass count / scan / write path,
 // 1 / 2 / 3 = single pass with tiles of 4 / 8 / 16 x 256 cells.
@@ -756,8 +756,7 @@ static int cu_count() {
     return cus;
 }
 
-// Per-lane running sums of the fused normal equations (k_normal_eq and
-// k_normal_eq_ring): NE<P>'s layout for every model but KB, whose 37 sums
+// Per-lane running sums of the fused normal equations (k_normal_eq): NE<P>'s layout for every model but KB, whose 37 sums
 // are built from powers of theta (below) and expanded to NE<8> at store().
 // FAST projection (reciprocal instead of per-point divisions) and fused
 // multiply-adds: the sums are held to 1e-10, not to the reference's
@@ -1008,128 +1007,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                 for (int u = 0; u < U; ++u) { x[u] = xn[u]; y[u] = yn[u]; z[u] = zn[u]; o[u] = on[u]; }
             }
         }
-    }
-    sums.store(parts + (size_t)blockIdx.x * K);
-}
-
-// k_normal_eq_ring: the same sums with the AoS point and observation streams
-// staged through a per-wave LDS ring by LDS-DMA (global_load_lds: the data
-// lands in LDS, no VGPR destination).  A wave takes 64 consecutive points per
-// step (1536 B of points as 16-B-per-lane pieces from 64 + 32 lanes + 1024 B
-// of observations as one 16-B-per-lane piece, in the bytes' order, so each lane then
-// reads its own point from LDS) and keeps the next S - 1 steps' loads in
-// flight.  (AoS points and observations on a 16-B boundary: the launcher
-// takes k_normal_eq otherwise.)  The register prefetch of k_normal_eq holds 10 VGPRs per step of
-// lookahead and the compiler's conservative vmcnt over its exec branches
-// waited for the next slot's loads mid-step (profiles/r03l_*); here the
-// lookahead costs LDS only and every wait is an explicit counted vmcnt.
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) const void gbl_void_t;
-constexpr int kRingSlot = 320;  // doubles per wave slot: 64 x (3 + 2)
-
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-    return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// waves per SIMD a ring of S slots leaves room for in the 160 KB of LDS
-// (one wave per SIMD per workgroup), capping the register target
-template <int W, int S>
-struct RingWaves {
-    static constexpr int lds = 4 * S * kRingSlot * 8 + 2048;
-    static constexpr int fit = (160 * 1024) / lds;
-    static constexpr int value = W < fit ? W : fit;
-};
-
-// s_waitcnt vmcnt(3 * ahead): every load but the `ahead` newest steps' three
-__device__ __forceinline__ void ring_wait(int ahead) {
-    switch (ahead) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    }
-}
-
-template <class TagT, int WAVES, int S, bool NTL>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RingWaves<WAVES, S>::value))) void k_normal_eq_ring(
-        acm_camera cam, size_t n, const double* __restrict__ pts, const double* __restrict__ obs,
-        int policy, double* __restrict__ parts) {
-    static_assert(S >= 2 && S <= 6, "ring depth");
-    using Acc = NeAccum<TagT>;
-    constexpr int K = Acc::K;
-    constexpr int kWaves = kBlock / 64;
-    __shared__ __attribute__((aligned(16))) double ring[kWaves][S][kRingSlot];
-    const Cam<double> c = make_cam<double>(cam);
-    Acc sums;
-    sums.init();
-    const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const size_t nw = (size_t)gridDim.x * kWaves;
-    // the ring takes an even number of points, so its last 16-B piece of
-    // points ends on the last point (24 nr = 16 x 3nr/2); an odd n's last
-    // point is added after the loop by plain loads
-    const size_t nr = n & ~(size_t)1;
-    const size_t nc = (nr + 63) / 64;  // 64-point steps
-    const size_t pbytes = nr * 24, obytes = nr * 16;
-    const char* pb = reinterpret_cast<const char*>(pts);
-    const char* ob = reinterpret_cast<const char*>(obs);
-    constexpr unsigned kAux = NTL ? 2u : 0u;  // nt
-    // one step's three 16-B-per-lane LDS-DMA loads into `slot`: points
-    // bytes [0, 1024) by all lanes and [1024, 1536) by lanes 0-31 (the
-    // others masked off: they neither read nor write), observations by all;
-    // pieces past the end of a stream read its first bytes instead (never
-    // accumulated).  (The 12-B form, global_load_lds_dwordx3, does not place
-    // lane l at base + 12 l on gfx950: measured wrong sums.)
-    auto issue = [&](int slot, size_t step) {
-        double* d = &ring[wid][slot][0];
-        const size_t p0 = step * 1536 + (size_t)lane * 16, p1 = p0 + 1024;
-        const size_t o0 = step * 1024 + (size_t)lane * 16;
-        const char* s0 = pb + (p0 + 16 <= pbytes ? p0 : 0);
-        const char* s1 = pb + (p1 + 16 <= pbytes ? p1 : 0);
-        const char* s2 = ob + (o0 + 16 <= obytes ? o0 : 0);
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)s0, (lds_void_t*)d, 16, 0, kAux);
-        if (lane < 32)
-            __builtin_amdgcn_global_load_lds((gbl_void_t*)s1, (lds_void_t*)(d + 128), 16, 0, kAux);
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)s2, (lds_void_t*)(d + 192), 16, 0, kAux);
-    };
-    size_t step = (size_t)blockIdx.x * kWaves + wid;
-#pragma unroll
-    for (int q = 0; q < S - 1; ++q) {
-        const size_t sq = step + (size_t)q * nw;
-        if (sq < nc) issue(q, sq);
-    }
-    int slot = 0;
-    for (; step < nc; step += nw) {
-        // the slot read one step ago takes the step S - 1 ahead (its LDS
-        // reads were consumed by that step's sums)
-        const size_t sn = step + (size_t)(S - 1) * nw;
-        if (sn < nc) issue(slot == 0 ? S - 1 : slot - 1, sn);
-        const size_t left = (nc - 1 - step) / nw;  // this wave's steps after this one
-        ring_wait(left < (size_t)(S - 1) ? (int)left : S - 1);
-        // the lane's 24 + 16 bytes, read in inline asm: a compiler-visible
-        // LDS read after an LDS-DMA gets a vmcnt(0) from the compiler (it
-        // cannot tell the slots apart), which would drain the ring
-        dbl2 xy, o;
-        double pz;
-        const double* d = &ring[wid][slot][0];
-        asm volatile(
-                "ds_read2_b64 %0, %3 offset1:1\n\t"
-                "ds_read_b64 %1, %3 offset:16\n\t"
-                "ds_read_b128 %2, %4\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=v"(xy), "=v"(pz), "=v"(o)
-                : "v"(lds_addr(d + 3 * lane)), "v"(lds_addr(d + 192 + 2 * lane))
-                : "memory");
-        if (step * 64 + lane < nr) sums.add(c, xy.x, xy.y, pz, make_double2(o.x, o.y), sent2);
-        slot = slot + 1 == S ? 0 : slot + 1;
-    }
-    if (nr != n && blockIdx.x == 0 && threadIdx.x == 0) {  // (no LDS-DMA in flight)
-        double x, y, z;
-        load_point<ACM_LAYOUT_AOS>(pts, n, n - 1, x, y, z);
-        sums.add(c, x, y, z, ld2<false>(obs + 2 * (n - 1)), sent2);
     }
     sums.store(parts + (size_t)blockIdx.x * K);
 }
@@ -2859,6 +2736,124 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n
     }
 }
 
+// Record form (r03, default): the same staging and evaluation, but each
+// point's terms sit in LDS as one 64-B record (AoS) that a lane reads whole
+// -- four 16-B broadcast reads -- one point ahead, alternating between two
+// register slots (no register copies, whose pending loads the compiler would
+// wait for).  The LDS form above reads the 8 values of a point inside the
+// evaluation, each read followed by its own lgkmcnt wait: ~4 LDS round trips
+// per (point, w) evaluation (VALU busy 0.59-0.72,
+// profiles/r03_fp64_kernels.md).  (Records in global memory read by
+// wave-uniform scalar loads measured 10.3 vs 8.7 ms: a scalar load from L2
+// outlasts one evaluation, and the 16 + 16 record SGPRs beside the 42 atan
+// coefficients spilled.)  Same per-point values and evaluation, so the sums
+// are bit-identical to the LDS form.
+// rec: r / z, z / r, 1 / r, fx x, fy y, cx - u, cy - v, mode (0: z > 0,
+// r > 0, both finite; 1: r2 < sqrt(EPS); 2: the general form, whose x, y, z,
+// u, v the evaluation reads back from the inputs).
+constexpr int kFovRec = 8;
+
+template <int LAYOUT>
+__global__ __launch_bounds__(kFovBlock) void k_fov_grid_rec(acm_camera cam, size_t n, size_t chunk,
+                                                            const double* __restrict__ pts,
+                                                            const double* __restrict__ obs,
+                                                            const double* __restrict__ table,
+                                                            double* __restrict__ parts) {
+    __shared__ __attribute__((aligned(16))) double srec[kFovBlock][kFovRec];
+    const int t = threadIdx.x;
+    const bool active = t < kFovGrid;
+    const double fx = cam.params[0], fy = cam.params[1], cx = cam.params[2], cy = cam.params[3];
+    double w = 1.0, tw2 = 0.0, rd0 = 0.0;
+    if (active) {
+        w = table[3 * t];
+        tw2 = table[3 * t + 1];
+        rd0 = table[3 * t + 2];
+    }
+    const double iw = 1.0 / w, itw2 = 1.0 / tw2;
+    const size_t b0 = (size_t)blockIdx.x * chunk;
+    const size_t b1 = b0 + chunk < n ? b0 + chunk : n;
+    double sum = 0.0, cnt = 0.0;
+    struct Rec { double q[kFovRec]; };
+    auto ldrec = [&](int k) {
+        Rec r;
+        const double2* p = reinterpret_cast<const double2*>(&srec[k][0]);
+#pragma unroll
+        for (int j = 0; j < kFovRec / 2; ++j) {
+            const double2 v = p[j];
+            r.q[2 * j] = v.x;
+            r.q[2 * j + 1] = v.y;
+        }
+        return r;
+    };
+    // the evaluation of k_fov_grid, operand for operand, on point i's record
+    auto eval = [&](const Rec& r, size_t i) -> double {
+        const double* q = r.q;
+        const double md = q[7];
+        double du, dv;
+        if (md != 2.0) {
+            double rd;
+            if (md == 0.0) {
+                const double a = tw2 * q[0];
+                const bool big = a > 1.0;
+                const double at = atan01(big ? itw2 * q[1] : a);
+                const double atan_wrd = big ? 1.5707963267948966 - at : at;  // :196
+                rd = atan_wrd * q[2] * iw;                                    // :205
+            } else {
+                rd = rd0;  // :200-203
+            }
+            du = fma(q[3], rd, q[5]);
+            dv = fma(q[4], rd, q[6]);
+        } else {
+            double x, y, z;
+            load_point<LAYOUT>(pts, n, i, x, y, z);
+            const double r2 = x * x + y * y, rr = sqrt(r2);
+            const double rd = fov_rd_general(tw2, rr, z, w, r2, rd0);
+            const double mx = x * rd, my = y * rd;
+            du = (fx * mx + cx) - obs[2 * i];
+            dv = (fy * my + cy) - obs[2 * i + 1];
+        }
+        const double d2 = fma(du, du, dv * dv);
+        return nr_range(d2) ? d2 * rsq_nr(d2) : sqrt(d2);
+    };
+    auto add = [&](double e) {
+        if (isfinite(e)) { sum += e; cnt += 1.0; }
+    };
+    for (size_t base = b0; base < b1; base += kFovBlock) {
+        __syncthreads();
+        const size_t i = base + t;
+        if (i < b1) {
+            double x, y, z;
+            load_point<LAYOUT>(pts, n, i, x, y, z);
+            const double r2 = x * x + y * y;  // :192-193
+            const double r = sqrt(r2);
+            const double u0 = obs[2 * i], v0 = obs[2 * i + 1];
+            const bool fast = z > 0.0 && r > 0.0 && z < INFINITY && r < INFINITY;
+            double2* o = reinterpret_cast<double2*>(&srec[t][0]);
+            o[0] = make_double2(fast ? r / z : 0.0, fast ? z / r : 0.0);
+            o[1] = make_double2(fast ? 1.0 / r : 0.0, fx * x);
+            o[2] = make_double2(fy * y, cx - u0);
+            o[3] = make_double2(cy - v0, r2 < kEpsSqrt ? 1.0 : (fast ? 0.0 : 2.0));
+        }
+        __syncthreads();
+        const int m = (int)(b1 - base < (size_t)kFovBlock ? b1 - base : (size_t)kFovBlock);
+        if (active) {
+            Rec A = ldrec(0);
+            int k = 0;
+            for (; k + 2 <= m; k += 2) {
+                const Rec B = ldrec(k + 1);
+                add(eval(A, base + k));
+                A = ldrec(k + 2 < m ? k + 2 : k + 1);
+                add(eval(B, base + k + 1));
+            }
+            if (k < m) add(eval(A, base + k));
+        }
+    }
+    if (active) {
+        parts[(size_t)blockIdx.x * (2 * kFovGrid) + t] = sum;
+        parts[(size_t)blockIdx.x * (2 * kFovGrid) + kFovGrid + t] = cnt;
+    }
+}
+
 // Chunk sums combined in block order (deterministic), one lane per column.
 // One workgroup per column: lane l sums chunks l, l + 256, ... and the lanes
 // combine in a fixed tree order (deterministic; a lane per column walking all
@@ -3532,19 +3527,6 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
             } else {
                 if (un >= 4) kern = ntl ? k_normal_eq<TagT, LAY, W, 3, true> : k_normal_eq<TagT, LAY, W, 3, false>;
             }
-            // 6, 7, 8: the LDS-DMA ring of 3, 4, 6 steps (AoS points; SoA
-            // takes 3)
-            const bool al16 = ((reinterpret_cast<uintptr_t>(points_3d) |
-                                reinterpret_cast<uintptr_t>(points_2d_obs)) & 15u) == 0;
-            if (LAY == ACM_LAYOUT_AOS && !al16 && un >= 6)
-                kern = ntl ? k_normal_eq<TagT, LAY, W, 3, true> : k_normal_eq<TagT, LAY, W, 3, false>;
-            else if constexpr (LAY == ACM_LAYOUT_AOS) {
-                if (un == 6) kern = ntl ? k_normal_eq_ring<TagT, W, 3, true> : k_normal_eq_ring<TagT, W, 3, false>;
-                if (un == 7) kern = ntl ? k_normal_eq_ring<TagT, W, 4, true> : k_normal_eq_ring<TagT, W, 4, false>;
-                if (un == 8) kern = ntl ? k_normal_eq_ring<TagT, W, 6, true> : k_normal_eq_ring<TagT, W, 6, false>;
-            } else if (un >= 6) {
-                kern = ntl ? k_normal_eq<TagT, LAY, W, 3, true> : k_normal_eq<TagT, LAY, W, 3, false>;
-            }
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
@@ -3763,7 +3745,10 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
     // the segment path would count every cell with the full Newton, so auto
     // keeps the single pass for it (1.32 vs 1.78 ms at 1e8 cells,
     // profiles/r03c_diag_sample.log)
-    if (mode < 0 && cam->model == ACM_RADTAN) mode = 2;
+    // ... and the speculative segment path beats both when (as for the
+    // sample camera) nothing or little is dropped: 0.99 vs 1.32 ms at 1e8
+    // cells (profiles/r03m_diag_sample.log)
+    if (mode < 0 && cam->model == ACM_RADTAN) mode = 4;
     const bool spec = mode == 4;
     if (mode < 0 || spec) {  // segment two-pass (default) / speculative segments
         const size_t nseg = (cells + kSegCells - 1) / kSegCells;
@@ -3938,7 +3923,7 @@ static size_t fov_blocks(size_t n) {
     static int cap = 0;
     if (!cap) {
         int per_cu = 0;
-        const void* k = reinterpret_cast<const void*>(k_fov_grid<ACM_LAYOUT_AOS, 1>);
+        const void* k = reinterpret_cast<const void*>(k_fov_grid_rec<ACM_LAYOUT_AOS>);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kFovBlock, 0) != hipSuccess ||
             per_cu <= 0) {
             (void)hipGetLastError();
@@ -3990,13 +3975,19 @@ ACM_API int acm_fov_grid_errors(const acm_camera* cam, size_t n, const double* p
     if (hipMemcpyAsync(table, fov_grid_table(), 3 * kFovGrid * sizeof(double),
                        hipMemcpyHostToDevice, s) != hipSuccess)
         return check_launch("acm_fov_grid_errors (table)");
+    const int fu = g_fov_unroll;
     auto go = [&](auto lay_c, auto u_c) {
-        hipLaunchKernelGGL((k_fov_grid<decltype(lay_c)::value, decltype(u_c)::value>), dim3(nb),
-                           dim3(kFovBlock), 0, s, *cam, n, chunk, points_3d, points_2d, table,
-                           parts);
+        constexpr int LAY = decltype(lay_c)::value, U = decltype(u_c)::value;
+        if (fu < 0) {  // record form (default)
+            hipLaunchKernelGGL((k_fov_grid_rec<LAY>), dim3(nb), dim3(kFovBlock), 0, s, *cam, n,
+                               chunk, points_3d, points_2d, table, parts);
+        } else {  // the LDS form, U points per lane step
+            hipLaunchKernelGGL((k_fov_grid<LAY, U>), dim3(nb), dim3(kFovBlock), 0, s, *cam, n,
+                               chunk, points_3d, points_2d, table, parts);
+        }
     };
     auto by_unroll = [&](auto lay_c) {
-        switch (g_fov_unroll) {
+        switch (fu) {
         case 2: go(lay_c, std::integral_constant<int, 2>{}); break;
         case 4: go(lay_c, std::integral_constant<int, 4>{}); break;
         default: go(lay_c, std::integral_constant<int, 1>{}); break;
@@ -4140,8 +4131,8 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_PROJECT_VARIANT, &g_project_variant, -1, 7, "variant must be -1 (auto) or 0..7"},
         {ACM_TUNE_RESIDUAL_NT, &g_residual_nt, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NE_WAVES, &g_ne_waves, 0, 4, "value must be 0 (per-model default), 1, 3 or 4"},
-        {ACM_TUNE_FOV_UNROLL, &g_fov_unroll, 1, 4, "value must be 1, 2 or 4"},
-        {ACM_TUNE_NE_UNROLL, &g_ne_unroll, 0, 8, "value must be 0 (per-model default) or 1..8"},
+        {ACM_TUNE_FOV_UNROLL, &g_fov_unroll, -1, 4, "value must be -1, 1, 2 or 4"},
+        {ACM_TUNE_NE_UNROLL, &g_ne_unroll, 0, 5, "value must be 0 (per-model default) or 1..5"},
         {ACM_TUNE_ALIGN_J, &g_align_j, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NT_LOADS, &g_nt_loads, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NT_LOADS_UNPROJECT, &g_nt_loads_unproject, -1, 1, "value must be -1..1"},
@@ -4161,7 +4152,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         if (k.key != key) continue;
         bool ok = value >= k.lo && value <= k.hi;
         if (key == ACM_TUNE_NE_WAVES) ok = ok && value != 2;
-        if (key == ACM_TUNE_FOV_UNROLL) ok = ok && value != 3;
+        if (key == ACM_TUNE_FOV_UNROLL) ok = ok && value != 0 && value != 3;
         if (key == ACM_TUNE_UNPROJECT_PPT) ok = ok && value != 0;
         if (!ok) return fail(ACM_ERR_INVALID_ARGUMENT, k.msg);
         return k.v->exchange(value);

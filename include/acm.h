@@ -426,13 +426,13 @@ ACM_API int acm_stream_synchronize(void *stream);
  * outputs exceed 64 MiB; non-temporal loads only if ACM_TUNE_NT_LOADS = 1).  ACM_TUNE_RESIDUAL_NT: non-temporal stores in
  * acm_residual_jacobian (-1 auto, 0 off = default, 1 on).  ACM_TUNE_NE_WAVES:
  * minimum waves per SIMD the normal-equations kernel is compiled for
- * (0 = per-model default, 1, 3, 4).  ACM_TUNE_FOV_UNROLL: points per lane step of the FOV
- * grid search (1 = default, 2, 4).  ACM_TUNE_NE_UNROLL: points per lane step
+ * (0 = per-model default, 1, 3, 4).  ACM_TUNE_FOV_UNROLL: the FOV grid search's kernel
+ * (-1 = auto (r03) = per-point 64-B records in LDS, each read whole one
+ * point ahead; 1 / 2 / 4 = the round-2 LDS kernel with 1 / 2 / 4 points per
+ * lane step).  ACM_TUNE_NE_UNROLL: points per lane step
  * of the normal-equations kernel (0 = per-model default, 1, 2; 3, 4, 5 = one
  * point per step with its loads issued 2, 3, 4 steps ahead; 4 and 5 are
- * Kannala-Brandt only, other models take 3; 6, 7, 8 = the LDS-DMA ring of
- * 3, 4, 6 steps of 64 points per wave, for AoS points and observations on a
- * 16-B boundary, 3 otherwise).
+ * Kannala-Brandt only, other models take 3).
  * ACM_TUNE_ALIGN_J: kernel of +Jacobian launches of acm_project /
  * acm_residual_jacobian: -1 = auto (default) = line-aligned store windows
  * through LDS, 0 = one point per lane with direct stores, 1 = aligned.
@@ -446,14 +446,15 @@ ACM_API int acm_stream_synchronize(void *stream);
  * stream synchronisation, 2 = on with the host spinning on a completion
  * word the kernel publishes; -1 = auto = 2.
  * ACM_TUNE_SAMPLE_FUSED: acm_sample_points' kernels.  -1 = auto (r03) = the
- * segment two-pass path (certified per-segment counts, offsets by a scan,
+ * speculative segment path (4, below) for RadTan, else the segment two-pass path (certified per-segment counts, offsets by a scan,
  * then a write pass with known offsets); 0 = the round-1 two-pass count /
  * scan / recompute-and-write path (tiles of 16 x 256 cells); 1 / 2 / 3 = the
  * single pass with a decoupled look-back, tiles of 2 / 4 / 8 x 256 cells
  * (round 1 mapped 1 / 2 / 3 to 4 / 8 / 16 x 256; changed in round 2); 4 =
- * speculative segments (r03): one pass writes every segment of 64 cells in
- * place as if nothing before it was dropped, a scan gives the true offsets
- * and a repair pass rewrites only the segments after the first drop.
+ * speculative segments (r03; auto for RadTan): one pass writes every
+ * segment of 64 cells in place as if nothing before it was dropped, a scan
+ * gives the true offsets and a repair pass rewrites only the segments after
+ * the first drop.
  * Outputs are identical for every value.
  * ACM_TUNE_SAMPLE_CERT: the segment path's host-certified keep regions
  * (-1 = auto = on; 0 = every segment counted cell by cell).  Same outputs.

@@ -148,8 +148,6 @@ def config3_ne_all(n):
         combos = [(0, 0, -1)] + [(wv, un, 1) for wv in (1, 3, 4) for un in (1, 2, 3)]
         if mid == 2:  # KB: loads 3 and 4 steps ahead too
             combos += [(wv, un, 1) for wv in (1, 3) for un in (4, 5)]
-        # 6 / 7 / 8: the LDS-DMA ring of 3 / 4 / 6 steps (AoS points)
-        combos += [(wv, un, 1) for wv in (1, 3, 4) for un in (6, 7, 8)]
         for rep in range(2):  # interleaved A/B: register target x lane step x nt loads
             for wv, un, nl in combos:
                 L.acm_set_tuning(_lib.TUNE_NE_WAVES, wv)
@@ -187,18 +185,21 @@ def config_fov(n_target):
     from apex_camera_models import _lib
     L = _lib.load()
     by = {}
-    for rep in range(2):  # interleaved A/B of the per-lane unroll
-        for u in (1, 2, 4):
+    # interleaved A/B: -1 = LDS records read one point ahead (r03), 1 / 2 /
+    # 4 = the round-2 LDS kernel
+    US = (-1, 1, 2, 4)
+    for rep in range(2):
+        for u in US:
             L.acm_set_tuning(_lib.TUNE_FOV_UNROLL, u)
             m.w = 1.0
             by.setdefault(u, []).append(timed(lambda: m.linear_estimation(xyz, uv), reps=3,
                                               warm=1))
             by.setdefault(("w", u), []).append(m.w)
-    L.acm_set_tuning(_lib.TUNE_FOV_UNROLL, 1)
+    L.acm_set_tuning(_lib.TUNE_FOV_UNROLL, -1)
     assert len({v[0] for k, v in by.items() if isinstance(k, tuple)}) == 1
-    ms = min(min(by[u]) for u in (1, 2, 4))
-    emit({"config": "fov", "what": "FOV grid unroll A/B",
-          "ms_by_unroll": {str(u): round(min(by[u]), 3) for u in (1, 2, 4)}})
+    ms = min(by[-1])
+    emit({"config": "fov", "what": "FOV grid kernel A/B",
+          "ms_by_unroll": {str(u): round(min(by[u]), 3) for u in US}})
     met = conversion.convert(src, "fov", xyz, uv)
     emit({"config": "fov", "what": "FOV grid-search linear estimation", "points": n,
           "ms": round(ms, 3), "evaluations_per_s": round(290 * n / ms / 1e3, 1), "w": m.w,
