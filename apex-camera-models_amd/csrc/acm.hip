@@ -59,6 +59,24 @@ struct Tag {
     using type = M<T>;
 };
 
+// sample_points' write kernels on a KB camera whose certified rays come from
+// the host's ray polynomials (kb_fit_ray): a tag of its own, so those
+// kernels hold only the polynomials' coefficients (the Newton form's
+// initial guess and sin / cos coefficients beside them spilled SGPRs)
+struct TagKbPoly : Tag<KannalaBrandt> {};
+template <class TagT>
+struct SampleTag {
+    using count = TagT;  // the count kernels' tag
+    static constexpr bool kb = std::is_same<TagT, Tag<KannalaBrandt>>::value;
+    static constexpr bool poly = false;
+};
+template <>
+struct SampleTag<TagKbPoly> {
+    using count = Tag<KannalaBrandt>;
+    static constexpr bool kb = true;
+    static constexpr bool poly = true;
+};
+
 template <class F>
 static int dispatch_model(int model, F&& f) {
     switch (model) {
@@ -135,6 +153,7 @@ struct CamArg : acm_camera {
     double ifx, ify;
     double uk[4];
     double kc[12];  // KB sample_points: certified kept interval + initial guess (Cam::kc)
+    double rp[2 * kRayPolyN];  // KB sample_points: certified-ray polynomials (Cam::rp)
 };
 
 template <class T>
@@ -151,6 +170,8 @@ __device__ __forceinline__ Cam<T> make_cam(const acm_camera& c) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) k.kc[i] = T(0);
     k.kc[0] = T(INFINITY);  // no certified interval (sample_points only)
+#pragma unroll
+    for (int i = 0; i < 2 * kRayPolyN; ++i) k.rp[i] = T(0);
     return k;
 }
 
@@ -170,6 +191,8 @@ __device__ __forceinline__ Cam<T> make_cam(const CamArg& c) {
     for (int i = 0; i < 4; ++i) k.uk[i] = c.uk[i];
 #pragma unroll
     for (int i = 0; i < 12; ++i) k.kc[i] = c.kc[i];
+#pragma unroll
+    for (int i = 0; i < 2 * kRayPolyN; ++i) k.rp[i] = c.rp[i];
     return k;
 }
 
@@ -1337,11 +1360,12 @@ __device__ __forceinline__ bool sample_cell(const Cam<double>& c, const Grid& g,
     using M = typename TagT::template type<double>;
     u = ((double)w.j + 0.5) * g.cw;  // :69
     v = ((double)w.i + 0.5) * g.ch;  // :70
-    if constexpr (std::is_same<TagT, Tag<KannalaBrandt>>::value) {
+    if constexpr (SampleTag<TagT>::kb) {
         // the keep decision taken exactly on the reference's theta, not read
         // off the polynomial-cos ray (KannalaBrandt::unproject_k)
         bool keep;
-        const uint8_t st = M::template unproject_k<true>(c, u, v, X, Y, Z, keep);
+        const uint8_t st =
+                M::template unproject_k<true, SampleTag<TagT>::poly>(c, u, v, X, Y, Z, keep);
         return st == ST_OK && keep;  // :91-94
     } else {
         const uint8_t st = M::unproject(c, u, v, X, Y, Z);
@@ -1507,8 +1531,10 @@ enum : int { SEG_UNKNOWN = 0, SEG_ALL = 1, SEG_NONE = 2 };
 struct SegCert {
     int on;
     int ig_ok;  // KB: ig[] fits theta*(ru) on [0, all_hi] for ray_certified: its Newton steps (1, 2) or 0
+    int rp_ok;  // KB: rp[] holds ray_certified's polynomials (kb_fit_ray)
     double all_lo, all_hi, none_lo, none_hi;
     double ig[9];  // KB: theta*(ru) ~= ru * sum ig[i] ru^(2i)
+    double rp[2 * kRayPolyN];  // KB: cos theta*, sin theta* / ru ~= sum rp[i] r2^i, sum rp[N + i] r2^i
 };
 
 // Rigorous bounds of r2 = mx^2 + my^2 over the cells [c0, c1] (inclusive,
@@ -2973,6 +2999,7 @@ static CamArg prep(acm_camera c, bool reference_newton = false) {
         a.uk[0] = NAN;  // fast Newton loops / FOV fast unprojection off
     for (int i = 0; i < 12; ++i) a.kc[i] = 0.0;
     a.kc[0] = INFINITY;  // no certified interval (set by acm_sample_points_ex for KB)
+    for (int i = 0; i < 2 * kRayPolyN; ++i) a.rp[i] = 0.0;
     return a;
 }
 
@@ -3130,6 +3157,80 @@ static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
     s.ig_ok = M * e0 * e0 <= 1e-17 ? 1 : (e0 <= 1e-5 && M * M * M * e0 * e0 * e0 * e0 <= 1e-13 ? 2 : 0);
 }
 
+// KB's certified-cell rays as polynomials in s = ru^2 on [0, all_hi^2]:
+// C(s) = cos(theta*(ru)), S(s) = sin(theta*(ru)) / ru (S(0) = 1: theta*'(0)
+// = 1).  Both are analytic in s (theta*(ru) / ru is an even analytic
+// function of ru), so degree 16 interpolants at Chebyshev nodes, solved in
+// long double (backward-stable elimination: the computed polynomials match
+// the node values to ~1e-18, and the Chebyshev nodes keep them as close in
+// between), reach rounding level; the error against long-double roots over
+// 4001 points of the interval must be <= 1e-13 (the rays are held to 1e-10)
+// or rp_ok stays 0 and ray_certified keeps its Newton form.
+static void kb_fit_ray(const double* p, SegCert& s) {
+    s.rp_ok = 0;
+    const long double k1 = p[4], k2 = p[5], k3 = p[6], k4 = p[7];
+    auto root = [&](long double ru) {
+        long double t = ru;
+        for (int i = 0; i < 80; ++i) {
+            const long double t2 = t * t;
+            const long double f = t * (1 + t2 * (k1 + t2 * (k2 + t2 * (k3 + t2 * k4)))) - ru;
+            const long double fp = 1 + t2 * (3 * k1 + t2 * (5 * k2 + t2 * (7 * k3 + t2 * 9 * k4)));
+            const long double d = f / fp;
+            t -= d;
+            if (std::fabs((double)d) < 1e-19) break;
+        }
+        return t;
+    };
+    auto cs = [&](long double sv, long double& C, long double& S) {
+        const long double ru = std::sqrt(sv);
+        const long double t = ru > 0 ? root(ru) : 0;
+        C = std::cos(t);
+        S = ru > 0 ? std::sin(t) / ru : 1;
+    };
+    const double R = s.all_hi;
+    if (!(R > 1e-3) || !(R < 1.5707963267948966)) return;
+    constexpr int N = kRayPolyN;
+    const long double Sm = (long double)R * R;
+    for (int which = 0; which < 2; ++which) {
+        long double A[N][N + 1];
+        for (int j = 0; j < N; ++j) {
+            const long double sj = Sm * (1 + std::cos(kPi * (j + 0.5) / N)) / 2;
+            long double C, S;
+            cs(sj, C, S);
+            long double pw = 1;
+            for (int i = 0; i < N; ++i, pw *= sj) A[j][i] = pw;
+            A[j][N] = which ? S : C;
+        }
+        for (int c = 0; c < N; ++c) {  // Gauss-Jordan with partial pivoting
+            int piv = c;
+            for (int r = c + 1; r < N; ++r)
+                if (std::fabs((double)A[r][c]) > std::fabs((double)A[piv][c])) piv = r;
+            for (int k = 0; k <= N; ++k) std::swap(A[c][k], A[piv][k]);
+            if (A[c][c] == 0) return;
+            for (int r = 0; r < N; ++r) {
+                if (r == c) continue;
+                const long double f = A[r][c] / A[c][c];
+                for (int k = c; k <= N; ++k) A[r][k] -= f * A[c][k];
+            }
+        }
+        for (int i = 0; i < N; ++i) s.rp[which * N + i] = (double)(A[i][N] / A[i][i]);
+    }
+    double err = 0.0;
+    for (int i = 0; i <= 4000; ++i) {
+        const double sv = (double)Sm * i / 4000.0;
+        double C = s.rp[N - 1], S = s.rp[2 * N - 1];
+        for (int k = N - 2; k >= 0; --k) {
+            C = std::fma(C, sv, s.rp[k]);
+            S = std::fma(S, sv, s.rp[N + k]);
+        }
+        long double Ct, St;
+        cs(sv, Ct, St);
+        err = std::fmax(err, std::fabs((double)(C - Ct)));
+        err = std::fmax(err, std::fabs((double)(S - St)) * std::sqrt(sv));  // X = mx S, |m| = ru
+    }
+    s.rp_ok = std::isfinite(err) && err <= 1e-13;
+}
+
 static SegCert kb_seg_cert(const double* p) {
     SegCert best{};
     best.all_lo = best.none_lo = INFINITY;
@@ -3146,7 +3247,10 @@ static SegCert kb_seg_cert(const double* p) {
             best = s;
         }
     }
-    if (best.on && best.all_hi > best.all_lo) kb_fit_initial_guess(p, best.ig[0], best);
+    if (best.on && best.all_hi > best.all_lo) {
+        kb_fit_initial_guess(p, best.ig[0], best);
+        kb_fit_ray(p, best);
+    }
     return best;
 }
 
@@ -3726,11 +3830,13 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
         // the certified kept interval + initial guess for ray_certified, in
         // every sample_points path alike (same rays whichever kernels run)
         const SegCert kc = kb_seg_cert_cached(cam->params);
-        if (kc.on && kc.ig_ok && kc.all_hi > kc.all_lo) {
+        if (kc.on && (kc.ig_ok || kc.rp_ok) && kc.all_hi > kc.all_lo) {
             ca.kc[0] = kc.all_lo;
             ca.kc[1] = kc.all_hi;
-            ca.kc[2] = kc.ig_ok;  // Newton steps of ray_certified
+            // ray_certified: 3 = the ray polynomials, else its Newton steps
+            ca.kc[2] = kc.rp_ok ? 3 : kc.ig_ok;
             for (int i = 0; i < 9; ++i) ca.kc[3 + i] = kc.ig[i];
+            for (int i = 0; i < 2 * kRayPolyN; ++i) ca.rp[i] = kc.rp[i];
         }
     }
     if (!cells) {  // nothing to launch: counts = [0 kept, 0 cells]
@@ -3750,6 +3856,13 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
     // cells (profiles/r03m_diag_sample.log)
     if (mode < 0 && cam->model == ACM_RADTAN) mode = 4;
     const bool spec = mode == 4;
+    // KB's certified rays from the ray polynomials (TagKbPoly) when the host
+    // fit holds; the count kernels take SampleTag<>::count either way
+    const bool poly = cam->model == ACM_KANNALA_BRANDT && ca.kc[2] == 3.0;
+    auto dispatch_sample = [&](auto&& f) -> int {
+        if (poly) return f(TagKbPoly{});
+        return dispatch_model(cam->model, f);
+    };
     if (mode < 0 || spec) {  // segment two-pass (default) / speculative segments
         const size_t nseg = (cells + kSegCells - 1) / kSegCells;
         const size_t nsb = (cells + kSegBlockCells - 1) / kSegBlockCells;
@@ -3757,8 +3870,9 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
         uint64_t* blk_sum = (uint64_t*)workspace + (nseg + 1) / 2;
         uint64_t* blk_off = blk_sum + nsb;
         const SegCert cert = seg_cert(*cam);
-        return dispatch_model(cam->model, [&](auto tag) -> int {
+        return dispatch_sample([&](auto tag) -> int {
             using TagT = decltype(tag);
+            using TagC = typename SampleTag<TagT>::count;
             // ACM_TUNE_SAMPLE_WRITE: segments per write wave and order
             // (-1 auto = 16 interleaved; 1 = 64 contiguous, 2 = 16
             // interleaved, 3 = 4 interleaved, 4 = 16 contiguous, 5 = 16
@@ -3784,7 +3898,7 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
                 wlaunch(k_seg_write<TagT, 16, true, false, true>, 16);
                 return check_launch("acm_sample_points");
             }
-            hipLaunchKernelGGL((k_seg_count<TagT>), dim3((unsigned)nsb), dim3(kBlock), 0, s, ca, g,
+            hipLaunchKernelGGL((k_seg_count<TagC>), dim3((unsigned)nsb), dim3(kBlock), 0, s, ca, g,
                                cells, cert, seg_cnt, blk_sum);
             hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, blk_sum, nsb, blk_off,
                                counts, (uint64_t)cells);
@@ -3800,7 +3914,7 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
         uint64_t* status = (uint64_t*)workspace + 1;
         if (hipMemsetAsync(workspace, 0, (nt + 1) * sizeof(uint64_t), s) != hipSuccess)
             return check_launch("acm_sample_points: workspace clear");
-        return dispatch_model(cam->model, [&](auto tag) -> int {
+        return dispatch_sample([&](auto tag) -> int {
             using TagT = decltype(tag);
             const int rr = mode == 1 ? 2 : mode == 2 ? 4 : 8;
             const size_t ntr = (cells + (size_t)kBlock * rr - 1) / ((size_t)kBlock * rr);
@@ -3814,10 +3928,10 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
     }
     uint64_t* cnt = (uint64_t*)workspace;
     uint64_t* off = cnt + nb;
-    return dispatch_model(cam->model, [&](auto tag) -> int {
+    return dispatch_sample([&](auto tag) -> int {
         using TagT = decltype(tag);
-        hipLaunchKernelGGL((k_sample_count<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, ca, g,
-                           cells, cnt);
+        hipLaunchKernelGGL((k_sample_count<typename SampleTag<TagT>::count>), dim3((unsigned)nb),
+                           dim3(kBlock), 0, s, ca, g, cells, cnt);
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, cnt, nb, off, counts,
                            (uint64_t)cells);
         hipLaunchKernelGGL((k_sample_write<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, ca, g,

@@ -281,6 +281,9 @@ __device__ __forceinline__ bool norm_below_1e6(T sq) {
     else return sqrt(sq) < T(1e-6);
 }
 
+// Coefficients of each of KB's certified-ray polynomials (degree 16 in r2)
+constexpr int kRayPolyN = 17;
+
 // Uniform camera parameters, converted once per thread from the kernel
 // argument (they stay in SGPRs: every lane reads the same values).
 template <class T>
@@ -296,9 +299,11 @@ struct Cam {
     T uk[4];
     // KB sample_points (kc[1] > 0 only there): cells whose ru lies in the
     // host-certified kept interval [kc[0], kc[1]] (acm.hip kb_seg_cert) take
-    // KannalaBrandt::ray_certified; kc[2] = its Newton steps (1 or 2),
-    // kc[3..11] = the initial-guess polynomial.
+    // KannalaBrandt::ray_certified; kc[2] = its Newton steps (1 or 2) from
+    // the initial-guess polynomial kc[3..11], or 3: the ray polynomials rp
+    // (cos theta*, sin theta* / ru in r2; acm.hip kb_fit_ray).
     T kc[12];
+    T rp[2 * kRayPolyN];
 };
 
 // (u - cx) / fx with fx uniform: RN(a / b) from the host's RN(1 / b) and the
@@ -780,8 +785,31 @@ struct KannalaBrandt {
     // ends below the clamp (ru = |m| < pi/2), so (sin(theta) m / ru,
     // cos(theta)) is a unit vector up to rounding (sin^2 + cos^2 = 1): no
     // normalisation -- within a few ulp of the reference's normalised ray.
+    //
+    // kc[2] = 3 (the default wherever the host fit holds, r03): the ray is
+    // read off two polynomials in r2 = ru^2 the host fits per camera on the
+    // certified interval, C(r2) = cos(theta*(ru)) and S(r2) = sin(theta*(ru))
+    // / ru (both analytic in r2; long-double roots at Chebyshev nodes, the
+    // error measured on 4001 points and required <= 1e-13, kb_fit_ray): X =
+    // mx S, Y = my S, Z = C -- 34 FMAs instead of the square root, the
+    // initial guess, the Newton step and sin / cos (~55 FP64 operations).
+    // POLY selects the form at compile time (the launcher picks the kernel
+    // by kc[2]): a kernel holding both forms' coefficients spilled SGPRs.
+    template <bool POLY>
     __device__ static __forceinline__ void ray_certified(const Cam<T>& c, T mx, T my, T r2, T& X,
                                                          T& Y, T& Z) {
+        if constexpr (POLY) {
+            T cp = c.rp[kRayPolyN - 1], sp = c.rp[2 * kRayPolyN - 1];
+#pragma unroll
+            for (int i = kRayPolyN - 2; i >= 0; --i) {
+                cp = fma(cp, r2, c.rp[i]);
+                sp = fma(sp, r2, c.rp[kRayPolyN + i]);
+            }
+            X = mx * sp;
+            Y = my * sp;
+            Z = cp;
+            return;
+        }
         const T k1 = c.p[4], k2 = c.p[5], k3 = c.p[6], k4 = c.p[7];
         const T ir = rsq_nr(r2);
         const T ru = r2 * ir;
@@ -838,7 +866,7 @@ struct KannalaBrandt {
     // the reference's; when it lies within 1e-11 of the threshold the pixel
     // runs the reference loop, so the comparison always sees either a theta
     // on the same side as the reference's or the reference's theta itself.
-    template <bool KEEP>
+    template <bool KEEP, bool POLY = false>
     __device__ static __forceinline__ uint8_t unproject_k(const Cam<T>& c, T u, T v, T& X, T& Y,
                                                           T& Z, bool& keep) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
@@ -862,7 +890,7 @@ struct KannalaBrandt {
             // only its ray is needed, to 1e-10: ray_certified
             if (r2 >= c.kc[0] * c.kc[0] * T(1 + 0x1p-30) &&
                 r2 <= c.kc[1] * c.kc[1] * T(1 - 0x1p-30)) {
-                ray_certified(c, mx, my, r2, X, Y, Z);
+                ray_certified<POLY>(c, mx, my, r2, X, Y, Z);
                 keep = true;
                 return ST_OK;
             }
