@@ -43,17 +43,29 @@ def main():
     n, m = a.points, a.cpu_points
     rows = []
 
-    def gpu_ms(fn, reps=10):
-        for _ in range(2):
-            fn()
+    def gpu_ms(fn, reps=10, blocks=3):
+        # warm for >= 50 ms of GPU work first: each row follows seconds of
+        # CPU-only oracle timing, and the GPU's clocks ramp back up over
+        # milliseconds (r03: a 2-call warm-up timed KB sample_points at 1.02
+        # ms against 0.80 ms in the kernel trace); then the fastest of
+        # `blocks` blocks of `reps` back-to-back calls (steady state)
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
+        t0 = time.perf_counter()
+        k = 0
+        while k < 3 or time.perf_counter() - t0 < 0.05:
             fn()
-        e1.record()
-        torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / reps
+            torch.cuda.synchronize()
+            k += 1
+        best = float("inf")
+        for _ in range(blocks):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            best = min(best, e0.elapsed_time(e1) / reps)
+        return best
 
     def cpu_s(fn, min_s=0.5):
         fn()  # warm (page in, first-touch)
