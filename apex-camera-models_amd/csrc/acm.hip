@@ -1034,90 +1034,85 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     sums.store(parts + (size_t)blockIdx.x * K);
 }
 
-// Epilogue of k_normal_eq in one launch (it was a column-sum kernel plus a
-// one-lane expansion kernel, 5.0 + 5.7 us per evaluation on config 3, now
-// 7.2 us; profiles/r01s7_lm_kernel_stats_{before,after}.csv): sum the per-workgroup partials
-// (nb x K, row-major) in a fixed order, then expand the structured sums ->
-// [JtJ full (P*P) | Jtr (P) | 0.5*rr | n_valid], one output per lane.
-// Lane t < R*K owns column t % K of the row group t / K (rows g, g + R, ...:
-// adjacent lanes read adjacent columns of one row); the R group sums of a
-// column are then added in group order by one lane.
-constexpr int kNeFinish = 1024;
-// flag != nullptr (the LM's host-polled path): after every result is out,
-// publish `seq` there with a system-scope release (out and flag are pinned
-// host memory the host spins on instead of synchronising the stream).
+// Epilogue of k_normal_eq: sum the per-workgroup partials (nb x K,
+// row-major) and expand the structured sums -> [JtJ full (P*P) | Jtr (P) |
+// 0.5*rr | n_valid].  Spread over the chip (r03): workgroup k < K sums
+// column k -- lane l takes rows l, l + 256, ... in order, then the wave
+// butterfly and the four waves in order, a fixed order so the result is
+// bit-reproducible -- and writes every output entry that is that sum (JtJ
+// is symmetric: up to two entries per sum; n_valid fills (cx, cx), (cy, cy)
+// and the last slot); workgroup K writes the structural zeros.  The
+// round-2 epilogue, one 1024-lane workgroup reading all nb x K partials,
+// took 6.5-7 us per evaluation (profiles/r03z_fp64_kernel_stats.csv); this
+// one cut the KB call 81.7 -> 78.7 us and DS's 74.8 -> 71.7 us
+// (profiles/r03u_ne_finish_ab_*.log).
+// ne_out_src(t): the sum output entry t comes from (-1: a structural zero)
 template <int P>
-__global__ __launch_bounds__(kNeFinish) void k_ne_finish(const double* __restrict__ parts, int nb,
-                                                         double* __restrict__ out,
-                                                         unsigned long long* __restrict__ flag,
-                                                         unsigned long long seq) {
+__device__ __forceinline__ int ne_out_src(int t) {
     using L = NE<P>;
     constexpr int D = L::D, K = L::K;
-    constexpr int R = kNeFinish / K;
-    __shared__ double red[R][K];
-    __shared__ double sm[K];
-    const int t = threadIdx.x;
-    if (t < R * K) {
-        // eight rows in flight per lane (the partials come back from other
-        // XCDs' L2 / MALL: a dependent chain of single loads took 11 us,
-        // this 7 us; 32 predicated loads per round trip measured 10 us)
-        const int k = t % K, g = t / K;
-        double a[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) a[u] = 0.0;
-        int b = g;
-        for (; b + 7 * R < nb; b += 8 * R) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = parts[(size_t)(b + u * R) * K + k];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) a[u] += v[u];
+    if (t < P * P) {
+        const int r = t / P, c = t % P;
+        const int i = r < c ? r : c, j = r < c ? c : r;
+        if (j >= 4) {
+            const int kj = j - 4;
+            if (i == 0) return L::A_DU + kj;
+            if (i == 1) return L::B_DV + kj;
+            if (i == 2) return L::DU + kj;
+            if (i == 3) return L::DV + kj;
+            const int ki = i - 4;  // upper triangle, row-major from (ki, ki)
+            return L::DDB + ki * D - ki * (ki - 1) / 2 + (kj - ki);
         }
-        for (; b < nb; b += R) a[0] += parts[(size_t)b * K + k];
-        red[g][k] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+        if (i == 0 && j == 0) return 0;
+        if (i == 0 && j == 2) return 1;
+        if (i == 1 && j == 1) return L::B2;
+        if (i == 1 && j == 3) return L::B1;
+        if (i == j) return K - 1;  // (2, 2), (3, 3): n_valid
+        return -1;
     }
-    __syncthreads();
-    if (t < K) {
+    if (t < P * P + P) return L::G + (t - P * P);
+    if (t == P * P + P) return K - 2;  // 0.5 * r.r
+    return K - 1;                      // n_valid
+}
+
+// SYS (the LM's host-polled path): each workgroup's results are made
+// visible at system scope before it ends, so the k_ne_publish that follows
+// in the stream can release the flag after all of them.
+template <int P, bool SYS>
+__global__ __launch_bounds__(kBlock) void k_ne_finish_cols(const double* __restrict__ parts, int nb,
+                                                           double* __restrict__ out) {
+    using L = NE<P>;
+    constexpr int K = L::K, NOUT = P * P + P + 2;
+    const int k = blockIdx.x;
+    __shared__ double sm[kBlock / 64];
+    __shared__ double s_sum;
+    if (k < K) {
         double a = 0.0;
-        for (int g = 0; g < R; ++g) a += red[g][t];
-        sm[t] = a;
-    }
-    __syncthreads();
-    if (t < P * P + P + 2) {
-        double v = 0.0;
-        if (t < P * P) {
-            // JtJ(i, j), i <= j: pinhole block (fx fy cx cy) and distortion block
-            const int r = t / P, c = t % P;
-            const int i = r < c ? r : c, j = r < c ? c : r;
-            if (j >= 4) {
-                const int kj = j - 4;
-                if (i == 0) v = sm[L::A_DU + kj];
-                else if (i == 1) v = sm[L::B_DV + kj];
-                else if (i == 2) v = sm[L::DU + kj];
-                else if (i == 3) v = sm[L::DV + kj];
-                else {
-                    const int ki = i - 4;  // upper triangle, row-major from (ki, ki)
-                    v = sm[L::DDB + ki * D - ki * (ki - 1) / 2 + (kj - ki)];
-                }
-            } else if (i == 0 && j == 0) v = sm[0];
-            else if (i == 0 && j == 2) v = sm[1];
-            else if (i == 1 && j == 1) v = sm[L::B2];
-            else if (i == 1 && j == 3) v = sm[L::B1];
-            else if (i == j) v = sm[K - 1];  // (2, 2), (3, 3): n_valid
-        } else if (t < P * P + P) {
-            v = sm[L::G + (t - P * P)];
-        } else if (t == P * P + P) {
-            v = 0.5 * sm[K - 2];
-        } else {
-            v = sm[K - 1];
-        }
-        out[t] = v;
-    }
-    if (flag) {
-        __threadfence_system();
+        for (int b = threadIdx.x; b < nb; b += kBlock) a += parts[(size_t)b * K + k];
+        a = wave_sum(a);
+        if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = a;
         __syncthreads();
-        if (t == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (threadIdx.x == 0) {
+            double t = 0.0;
+            for (int w = 0; w < kBlock / 64; ++w) t += sm[w];
+            s_sum = t;
+        }
+        __syncthreads();
+        const double S = s_sum;
+        for (int t = threadIdx.x; t < NOUT; t += kBlock)
+            if (ne_out_src<P>(t) == k) out[t] = t == P * P + P ? 0.5 * S : S;
+    } else {
+        for (int t = threadIdx.x; t < NOUT; t += kBlock)
+            if (ne_out_src<P>(t) < 0) out[t] = 0.0;
     }
+    if (SYS) __threadfence_system();
+}
+
+// The LM's host-polled path after k_ne_finish_cols: every result is out
+// (stream order), publish `seq` with a system-scope release.
+__global__ void k_ne_publish(unsigned long long* __restrict__ flag, unsigned long long seq) {
+    __threadfence_system();
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ----------------------------------------------------- reprojection stats
@@ -3592,7 +3587,7 @@ ACM_API size_t acm_normal_equations_workspace_size(int model, size_t n) {
 
 extern "C++" {
 namespace acm {
-// flag / seq: see k_ne_finish (the LM's polled path in solver.hip)
+// flag / seq: see k_ne_finish_cols / k_ne_publish (the LM's polled path in solver.hip)
 int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                           const double* points_2d_obs, int invalid_policy, double* result,
                           void* workspace, size_t workspace_bytes, void* stream,
@@ -3645,8 +3640,14 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
         };
         if (layout == ACM_LAYOUT_AOS) by_waves(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else by_waves(std::integral_constant<int, ACM_LAYOUT_SOA>{});
-        hipLaunchKernelGGL(k_ne_finish<P>, dim3(1), dim3(kNeFinish), 0, s, parts, nb, result, flag,
-                           seq);
+        if (flag) {
+            hipLaunchKernelGGL((k_ne_finish_cols<P, true>), dim3(NE<P>::K + 1), dim3(kBlock), 0, s,
+                               parts, nb, result);
+            hipLaunchKernelGGL(k_ne_publish, dim3(1), dim3(1), 0, s, flag, seq);
+        } else {
+            hipLaunchKernelGGL((k_ne_finish_cols<P, false>), dim3(NE<P>::K + 1), dim3(kBlock), 0, s,
+                               parts, nb, result);
+        }
         return check_launch("acm_normal_equations");
     });
 }
