@@ -165,26 +165,28 @@ def lib_sha256():
 
 
 def load_traffic(workload, n):
-    """HBM bytes per launch from the newest committed rocprofv3 PMC summary
-    of this exact workload (profiles/*pmc*.json, profiles/collect_pmc.py),
-    used only if it was collected on this very libacm.so (its sha256 is
-    recorded in the summary); otherwise traffic is null and the source says
-    why.  Returns (bytes or None, source description)."""
+    """HBM bytes per launch from a committed rocprofv3 PMC summary of this
+    exact workload (profiles/*pmc*.json, profiles/collect_pmc.py), used only
+    if it was collected on this very libacm.so (its sha256 is recorded in
+    the summary) or on a rebuild of the very same sources and build
+    variant; otherwise traffic is null and the source says why.  Among
+    several summaries the one matching this library wins, whatever its
+    file name.  Returns (bytes or None, source description)."""
     import glob
-    best = None
+    cands = []
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
         if d.get("workload") == workload and int(d.get("points", -1)) == n:
-            best = (p, d)
-    if best is None:
+            cands.append((p, d))
+    if not cands:
         return None, "no PMC summary for this workload"
-    p, d = best
-    rel = os.path.relpath(p, ROOT)
-    if d.get("libacm_sha256") == lib_sha256():
-        return d["hbm_bytes_per_launch"], rel
+    sha = lib_sha256()
+    for p, d in reversed(cands):
+        if d.get("libacm_sha256") == sha:
+            return d["hbm_bytes_per_launch"], os.path.relpath(p, ROOT)
     # hipcc output is not byte-reproducible: accept a rebuild of the very
     # same sources (and build recipe), provided the library is newer than
     # every source file (so it was built from them)
@@ -193,11 +195,14 @@ def load_traffic(workload, n):
     # and acm_version() (which lists the defines) -- a counter file from a
     # diagnostic build is never reported for the production library.
     from apex_camera_models import _buildinfo, _lib
-    src_ok = d.get("libacm_source_sha256") is not None and \
-        d["libacm_source_sha256"] == _lib.source_sha256() and \
-        d.get("libacm_identity") == _buildinfo.lib_identity(_lib.LIB_PATH)
-    if src_ok and os.path.getmtime(_lib.LIB_PATH) >= _latest_source_mtime():
-        return d["hbm_bytes_per_launch"], rel + " (same libacm sources, rebuilt library)"
+    src = _lib.source_sha256()
+    ident = _buildinfo.lib_identity(_lib.LIB_PATH)
+    fresh = os.path.getmtime(_lib.LIB_PATH) >= _latest_source_mtime()
+    for p, d in reversed(cands):
+        if fresh and d.get("libacm_source_sha256") == src and d.get("libacm_identity") == ident:
+            return d["hbm_bytes_per_launch"], \
+                os.path.relpath(p, ROOT) + " (same libacm sources, rebuilt library)"
+    rel = os.path.relpath(cands[-1][0], ROOT)
     return None, f"{rel} was collected on another libacm.so build (stale): not reported"
 
 

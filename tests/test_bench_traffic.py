@@ -90,3 +90,18 @@ def test_other_workload_or_size(root):
     _write(root, libacm_sha256=bench.lib_sha256())
     assert bench.load_traffic(WL, 1_000_000)[0] is None
     assert bench.load_traffic("kb_project_f64_aos", 10_000_000)[0] is None
+
+
+def test_matching_summary_wins_over_a_later_named_stale_one(root):
+    """Several summaries of the workload: the one collected on this library
+    is reported even when a stale one sorts after it by file name."""
+    prof = root / "profiles"
+    prof.mkdir(exist_ok=True)
+    base = {"workload": WL, "points": 10_000_000}
+    (prof / "a_pmc_match.json").write_text(json.dumps(
+        {**base, "hbm_bytes_per_launch": 1.7e9, "libacm_sha256": bench.lib_sha256()}))
+    (prof / "z_pmc_stale.json").write_text(json.dumps(
+        {**base, "hbm_bytes_per_launch": 9.9e9, "libacm_sha256": "0" * 64,
+         "libacm_source_sha256": "1" * 64}))
+    t, src = bench.load_traffic(WL, 10_000_000)
+    assert t == 1.7e9 and src.endswith("a_pmc_match.json")
