@@ -278,7 +278,9 @@ static std::atomic<int> g_nt_loads{-1};
 // 1): beside the non-temporal ray stores they measured 2-25% slower for
 // every model (profiles/r01_diag_ntl.log).
 static std::atomic<int> g_nt_loads_unproject{-1};
-// FOV grid search: points per lane step (1 = default, 2, 4).
+// FOV grid search kernel: -1 = the point-lane form (default), 0 = the
+// per-point LDS record form, 1 / 2 / 4 = the LDS form with that many points
+// per lane step.
 static std::atomic<int> g_fov_unroll{-1};
 // sample_points: -1 = auto = single pass with decoupled look-back and the
 // per-model tile (SampleR), 0 = the two-pass count / scan / write path,
@@ -2875,6 +2877,164 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid_rec(acm_camera cam, size
     }
 }
 
+// Point-lane form (r03, default): the transpose of the two forms above.  A
+// lane owns P points of a 64 P-point group (their terms in registers, no LDS
+// in the loop) and every wave walks the 290 grid values with the per-w
+// constants as wave-uniform scalar loads; per grid value the wave's P x 64
+// errors are summed lane-serially, then by the xor butterfly (the same bits
+// in every lane), and the finite count is a ballot popcount.  Lane l of a
+// wave keeps the running totals of grid values l, l + 64, ... in registers.
+// Every lane is busy (the grid-lane forms run 290 of 320 lanes) and the P
+// evaluations of a lane are independent chains.  The terms are those of the
+// forms above, bit for bit; only the summation order differs (the grid sums
+// are held to 1e-12 of the serial reference, counts exact).  Groups are split
+// evenly over all waves of a grid sized to the resident workgroups.
+// table: w, 2 tan(w/2), 2 tan(w/2) / w (3 per grid value), then 1 / w and
+// 1 / (2 tan(w/2)) (2 per grid value; the host's IEEE divisions, the same
+// bits as the device's).
+constexpr int kFovPlBlock = 256;
+constexpr int kFovPlP = 3;
+
+template <int LAYOUT, int P>
+__global__ __launch_bounds__(kFovPlBlock) void k_fov_grid_pl(acm_camera cam, size_t n,
+                                                             const double* __restrict__ pts,
+                                                             const double* __restrict__ obs,
+                                                             const double* __restrict__ table,
+                                                             double* __restrict__ parts) {
+    constexpr int kWaves = kFovPlBlock / 64, kGroup = 64 * P, kWB = (kFovGrid + 63) / 64;
+    __shared__ double s_sum[kWaves][kFovGrid], s_cnt[kWaves][kFovGrid];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double fx = cam.params[0], fy = cam.params[1], cx = cam.params[2], cy = cam.params[3];
+    const size_t groups = (n + kGroup - 1) / kGroup;
+    const size_t nw = (size_t)gridDim.x * kWaves, gw = (size_t)blockIdx.x * kWaves + wv;
+    const size_t g0 = groups * gw / nw, g1 = groups * (gw + 1) / nw;
+    double acc[kWB];
+    uint32_t accn[kWB];
+#pragma unroll
+    for (int b = 0; b < kWB; ++b) {
+        acc[b] = 0.0;
+        accn[b] = 0;
+    }
+    for (size_t g = g0; g < g1; ++g) {
+        // Per point: r / z, z / r, 1 / r, fx x, fy y, cx - u, cy - v and fl.
+        // Branch-free evaluation rd = fma(rd0, fl, atan * (1 / r) / w):
+        // z > 0, r > 0, both finite -> fl = 0 (the atan form); r2 < sqrt(EPS)
+        // -> 1 / r = 0, fl = 1 (rd = rd0, :200-203); anything else -> the
+        // general form (OCML atan2, x, y, z, u, v read back) on a slow path
+        // taken by the groups that hold such a point; past the end -> cx - u
+        // = NaN, so the error is not finite and is not counted.
+        double rz[P], zr[P], ir[P], ax[P], ay[P], bx[P], by[P], fl[P];
+        bool gen = false;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const size_t i = g * kGroup + (size_t)j * 64 + lane;
+            rz[j] = zr[j] = ir[j] = ax[j] = ay[j] = by[j] = fl[j] = 0.0;
+            bx[j] = __builtin_nan("");
+            if (i < n) {
+                double x, y, z;
+                load_point<LAYOUT>(pts, n, i, x, y, z);
+                const double r2 = x * x + y * y;  // fov.rs:192-193
+                const double r = sqrt(r2);
+                const double u0 = obs[2 * i], v0 = obs[2 * i + 1];
+                const bool fast = z > 0.0 && r > 0.0 && z < INFINITY && r < INFINITY;
+                const bool small = r2 < kEpsSqrt;
+                rz[j] = fast ? r / z : 0.0;
+                zr[j] = fast ? z / r : 0.0;
+                ir[j] = fast && !small ? 1.0 / r : 0.0;
+                fl[j] = small ? 1.0 : 0.0;
+                ax[j] = fx * x; ay[j] = fy * y;
+                bx[j] = cx - u0; by[j] = cy - v0;
+                gen = gen || (!small && !fast);
+            }
+        }
+        auto walk = [&](auto gen_c) {
+            constexpr bool GEN = decltype(gen_c)::value;
+#pragma unroll
+            for (int b = 0; b < kWB; ++b) {
+                const int wl_end = kFovGrid - b * 64 < 64 ? kFovGrid - b * 64 : 64;
+                for (int wl = 0; wl < wl_end; ++wl) {
+                    const int k = b * 64 + wl;
+                    const double w = table[3 * k], tw2 = table[3 * k + 1],
+                                 rd0 = table[3 * k + 2];
+                    const double iw = table[3 * kFovGrid + 2 * k];
+                    const double itw2 = table[3 * kFovGrid + 2 * k + 1];
+                    double d2[P], e[P];
+                    bool slow = false;
+#pragma unroll
+                    for (int j = 0; j < P; ++j) {
+                        // the evaluation of k_fov_grid, operand for operand
+                        const double a = tw2 * rz[j];
+                        const bool big = a > 1.0;
+                        const double at = atan01(big ? itw2 * zr[j] : a);
+                        const double atan_wrd = big ? 1.5707963267948966 - at : at;  // :196
+                        const double rd = fma(rd0, fl[j], atan_wrd * ir[j] * iw);    // :205
+                        const double du = fma(ax[j], rd, bx[j]), dv = fma(ay[j], rd, by[j]);
+                        d2[j] = fma(du, du, dv * dv);
+                        e[j] = d2[j] * rsq_nr(d2[j]);  // :211-213
+                        slow = slow || !nr_range(d2[j]);
+                    }
+                    if (GEN) {
+#pragma unroll
+                        for (int j = 0; j < P; ++j) {
+                            const size_t i = g * kGroup + (size_t)j * 64 + lane;
+                            if (i < n && fl[j] == 0.0 && ir[j] == 0.0) {
+                                double x, y, z;
+                                load_point<LAYOUT>(pts, n, i, x, y, z);
+                                const double r2 = x * x + y * y, rr = sqrt(r2);
+                                const double rdg = fov_rd_general(tw2, rr, z, w, r2, rd0);
+                                const double du = (fx * (x * rdg) + cx) - obs[2 * i];
+                                const double dv = (fy * (y * rdg) + cy) - obs[2 * i + 1];
+                                d2[j] = fma(du, du, dv * dv);
+                                e[j] = d2[j] * rsq_nr(d2[j]);
+                                slow = slow || !nr_range(d2[j]);
+                            }
+                        }
+                    }
+                    if (slow) {  // 0, huge or NaN: the IEEE sqrt
+#pragma unroll
+                        for (int j = 0; j < P; ++j)
+                            if (!nr_range(d2[j])) e[j] = sqrt(d2[j]);
+                    }
+                    double s = 0.0;
+                    uint32_t c = 0;
+#pragma unroll
+                    for (int j = 0; j < P; ++j) {
+                        const bool f = isfinite(e[j]);
+                        s += f ? e[j] : 0.0;
+                        c += (uint32_t)__popcll(__ballot(f));
+                    }
+                    s = wave_sum(s);
+                    if (lane == wl) {
+                        acc[b] += s;
+                        accn[b] += c;
+                    }
+                }
+            }
+        };
+        if (__ballot(gen)) walk(std::true_type{});
+        else walk(std::false_type{});
+    }
+#pragma unroll
+    for (int b = 0; b < kWB; ++b) {
+        const int k = b * 64 + lane;
+        if (k < kFovGrid) {
+            s_sum[wv][k] = acc[b];
+            s_cnt[wv][k] = (double)accn[b];
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kFovGrid; k += kFovPlBlock) {
+        double s = s_sum[0][k], c = s_cnt[0][k];
+#pragma unroll
+        for (int v = 1; v < kWaves; ++v) {
+            s += s_sum[v][k];
+            c += s_cnt[v][k];
+        }
+        parts[(size_t)blockIdx.x * (2 * kFovGrid) + k] = s;
+        parts[(size_t)blockIdx.x * (2 * kFovGrid) + kFovGrid + k] = c;
+    }
+}
+
 // Chunk sums combined in block order (deterministic), one lane per column.
 // One workgroup per column: lane l sums chunks l, l + 256, ... and the lanes
 // combine in a fixed tree order (deterministic; a lane per column walking all
@@ -4034,25 +4194,37 @@ ACM_API int acm_linear_system_qr(const acm_camera* cam, size_t n, const double* 
 // in solver.hip (acm_fov_grid_select).
 // Chunks of >= 256 points, at most the workgroups resident at once (a grid
 // of 1.33 rounds left a third of the chip idle for the last round).
-static size_t fov_blocks(size_t n) {
-    static int cap = 0;
-    if (!cap) {
-        int per_cu = 0;
-        const void* k = reinterpret_cast<const void*>(k_fov_grid_rec<ACM_LAYOUT_AOS>);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kFovBlock, 0) != hipSuccess ||
-            per_cu <= 0) {
-            (void)hipGetLastError();
-            per_cu = 4;
-        }
-        cap = std::min(kFovMaxBlocks, per_cu * cu_count());
+static int fov_cap(const void* k, int block) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, block, 0) != hipSuccess ||
+        per_cu <= 0) {
+        (void)hipGetLastError();
+        per_cu = 4;
     }
+    return std::min(kFovMaxBlocks, per_cu * cu_count());
+}
+// the grid-lane forms: chunks of >= 256 points
+static size_t fov_blocks_rec(size_t n) {
+    static const int cap = fov_cap(reinterpret_cast<const void*>(k_fov_grid_rec<ACM_LAYOUT_AOS>),
+                                   kFovBlock);
     size_t nb = (n + kBlock - 1) / kBlock;
     if (nb > (size_t)cap) nb = cap;
     return nb ? nb : 1;
 }
+// the point-lane form: >= one group per wave
+static size_t fov_blocks_pl(size_t n) {
+    static const int cap = fov_cap(
+        reinterpret_cast<const void*>(k_fov_grid_pl<ACM_LAYOUT_AOS, kFovPlP>), kFovPlBlock);
+    const size_t per_block = (size_t)kFovPlBlock * kFovPlP;
+    size_t nb = (n + per_block - 1) / per_block;
+    if (nb > (size_t)cap) nb = cap;
+    return nb ? nb : 1;
+}
+// the partial-sum rows of the workspace: enough for either form
+static size_t fov_blocks(size_t n) { return std::max(fov_blocks_rec(n), fov_blocks_pl(n)); }
 
 static const double* fov_grid_table() {
-    static double table[3 * kFovGrid];
+    static double table[5 * kFovGrid];
     static const bool init = [] {
         for (int i = 10; i < 10 + kFovGrid; ++i) {
             const double w = (double)i / 100.0;          // :180
@@ -4060,6 +4232,8 @@ static const double* fov_grid_table() {
             table[3 * (i - 10)] = w;
             table[3 * (i - 10) + 1] = 2.0 * tan_w_half;          // :196, exact
             table[3 * (i - 10) + 2] = 2.0 * tan_w_half / w;      // :202
+            table[3 * kFovGrid + 2 * (i - 10)] = 1.0 / w;
+            table[3 * kFovGrid + 2 * (i - 10) + 1] = 1.0 / (2.0 * tan_w_half);
         }
         return true;
     }();
@@ -4068,7 +4242,7 @@ static const double* fov_grid_table() {
 }
 
 ACM_API size_t acm_fov_grid_workspace_size(size_t n) {
-    return (fov_blocks(n) * 2 * kFovGrid + 3 * kFovGrid) * sizeof(double);
+    return (fov_blocks(n) * 2 * kFovGrid + 5 * kFovGrid) * sizeof(double);
 }
 
 ACM_API int acm_fov_grid_errors(const acm_camera* cam, size_t n, const double* points_3d,
@@ -4083,17 +4257,20 @@ ACM_API int acm_fov_grid_errors(const acm_camera* cam, size_t n, const double* p
     if (workspace_bytes < acm_fov_grid_workspace_size(n))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "FOV grid workspace too small");
     hipStream_t s = (hipStream_t)stream;
-    const size_t nb = fov_blocks(n);
+    const int fu = g_fov_unroll;
+    const size_t nb = fu < 0 ? fov_blocks_pl(n) : fov_blocks_rec(n);
     const size_t chunk = (n + nb - 1) / nb;
     double* parts = (double*)workspace;
-    double* table = parts + nb * 2 * kFovGrid;
-    if (hipMemcpyAsync(table, fov_grid_table(), 3 * kFovGrid * sizeof(double),
+    double* table = parts + fov_blocks(n) * 2 * kFovGrid;
+    if (hipMemcpyAsync(table, fov_grid_table(), 5 * kFovGrid * sizeof(double),
                        hipMemcpyHostToDevice, s) != hipSuccess)
         return check_launch("acm_fov_grid_errors (table)");
-    const int fu = g_fov_unroll;
     auto go = [&](auto lay_c, auto u_c) {
         constexpr int LAY = decltype(lay_c)::value, U = decltype(u_c)::value;
-        if (fu < 0) {  // record form (default)
+        if (fu < 0) {  // point-lane form (default)
+            hipLaunchKernelGGL((k_fov_grid_pl<LAY, kFovPlP>), dim3(nb), dim3(kFovPlBlock), 0, s,
+                               *cam, n, points_3d, points_2d, table, parts);
+        } else if (fu == 0) {  // record form
             hipLaunchKernelGGL((k_fov_grid_rec<LAY>), dim3(nb), dim3(kFovBlock), 0, s, *cam, n,
                                chunk, points_3d, points_2d, table, parts);
         } else {  // the LDS form, U points per lane step
@@ -4246,7 +4423,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_PROJECT_VARIANT, &g_project_variant, -1, 7, "variant must be -1 (auto) or 0..7"},
         {ACM_TUNE_RESIDUAL_NT, &g_residual_nt, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NE_WAVES, &g_ne_waves, 0, 4, "value must be 0 (per-model default), 1, 3 or 4"},
-        {ACM_TUNE_FOV_UNROLL, &g_fov_unroll, -1, 4, "value must be -1, 1, 2 or 4"},
+        {ACM_TUNE_FOV_UNROLL, &g_fov_unroll, -1, 4, "value must be -1, 0, 1, 2 or 4"},
         {ACM_TUNE_NE_UNROLL, &g_ne_unroll, 0, 5, "value must be 0 (per-model default) or 1..5"},
         {ACM_TUNE_ALIGN_J, &g_align_j, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NT_LOADS, &g_nt_loads, -1, 1, "value must be -1..1"},
@@ -4267,7 +4444,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         if (k.key != key) continue;
         bool ok = value >= k.lo && value <= k.hi;
         if (key == ACM_TUNE_NE_WAVES) ok = ok && value != 2;
-        if (key == ACM_TUNE_FOV_UNROLL) ok = ok && value != 0 && value != 3;
+        if (key == ACM_TUNE_FOV_UNROLL) ok = ok && value != 3;
         if (key == ACM_TUNE_UNPROJECT_PPT) ok = ok && value != 0;
         if (!ok) return fail(ACM_ERR_INVALID_ARGUMENT, k.msg);
         return k.v->exchange(value);

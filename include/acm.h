@@ -427,9 +427,12 @@ ACM_API int acm_stream_synchronize(void *stream);
  * acm_residual_jacobian (-1 auto, 0 off = default, 1 on).  ACM_TUNE_NE_WAVES:
  * minimum waves per SIMD the normal-equations kernel is compiled for
  * (0 = per-model default, 1, 3, 4).  ACM_TUNE_FOV_UNROLL: the FOV grid search's kernel
- * (-1 = auto (r03) = per-point 64-B records in LDS, each read whole one
- * point ahead; 1 / 2 / 4 = the round-2 LDS kernel with 1 / 2 / 4 points per
- * lane step).  ACM_TUNE_NE_UNROLL: points per lane step
+ * (-1 = auto (r03) = the point-lane form: lanes own points, every wave
+ * walks the grid, sums by wave butterfly -- another summation order, counts
+ * identical, sums within ~1e-15; 0 = per-point 64-B records in LDS, each
+ * read whole one point ahead (the r03 record form, -1 until r03's point-lane
+ * form); 1 / 2 / 4 = the round-2 LDS kernel with 1 / 2 / 4 points per lane
+ * step).  acm_fov_grid_workspace_size grew by 2 x 290 doubles (r03).  ACM_TUNE_NE_UNROLL: points per lane step
  * of the normal-equations kernel (0 = per-model default, 1, 2; 3, 4, 5 = one
  * point per step with its loads issued 2, 3, 4 steps ahead; 4 and 5 are
  * Kannala-Brandt only, other models take 3).

@@ -153,7 +153,7 @@ def test_tuning_knobs_validate_and_restore():
     cases = {_lib.TUNE_PROJECT_VARIANT: ([-1, 0, 1, 2, 3, 4, 5, 6, 7], [-2, 8]),
              _lib.TUNE_RESIDUAL_NT: ([-1, 0, 1], [2]),
              _lib.TUNE_NE_WAVES: ([0, 1, 3, 4], [2, 5]),
-             _lib.TUNE_FOV_UNROLL: ([-1, 1, 2, 4], [0, 3, 5, 8]),
+             _lib.TUNE_FOV_UNROLL: ([-1, 0, 1, 2, 4], [-2, 3, 5, 8]),
              _lib.TUNE_NE_UNROLL: ([0, 1, 2, 3, 4, 5], [6, -1]),
              _lib.TUNE_ALIGN_J: ([-1, 0, 1], [2]),
              _lib.TUNE_NT_LOADS: ([-1, 0, 1], [2]),

@@ -274,22 +274,25 @@ def test_fov_grid_errors_match_oracle(n):
 
 @pytest.mark.parametrize("n", [1, 7, 320 * 3 + 5, 20_001])
 def test_fov_grid_kernels_bit_identical(n):
-    """The record form of the grid search (default) and the round-2 LDS
-    form (1, 2, 4 points per lane step) evaluate the same per-point
-    terms in the same order: identical sums and counts, including the
-    special points (on the axis, z = 0, NaN, r ~ 0)."""
+    """The record form of the grid search (0) and the round-2 LDS form (1, 2,
+    4 points per lane step) evaluate the same per-point terms in the same
+    order: identical sums and counts, including the special points (on the
+    axis, z = 0, NaN, r ~ 0).  The point-lane form (the default, -1) sums the
+    same terms in another order: identical counts, sums within 1e-12."""
     from apex_camera_models import _lib
     L = _lib.load()
     p, xyz, uv = _fov_data(n, 90 + n, noise=0.7)
     res = {}
     try:
-        for u in (-1, 1, 2, 4):
+        for u in (-1, 0, 1, 2, 4):
             L.acm_set_tuning(_lib.TUNE_FOV_UNROLL, u)
             res[u] = _fov_grid_gpu(p, xyz, uv)
     finally:
         L.acm_set_tuning(_lib.TUNE_FOV_UNROLL, -1)
     for u in (1, 2, 4):
-        assert np.array_equal(res[u][0], res[-1][0]) and np.array_equal(res[u][1], res[-1][1]), u
+        assert np.array_equal(res[u][0], res[0][0]) and np.array_equal(res[u][1], res[0][1]), u
+    assert np.array_equal(res[-1][1], res[0][1])
+    assert np.all(np.abs(res[-1][0] - res[0][0]) <= 1e-12 * np.abs(res[0][0]))
 
 
 @pytest.mark.parametrize("w_true", [0.37, 0.93, 1.5, 2.41])

@@ -185,9 +185,9 @@ def config_fov(n_target):
     from apex_camera_models import _lib
     L = _lib.load()
     by = {}
-    # interleaved A/B: -1 = LDS records read one point ahead (r03), 1 / 2 /
-    # 4 = the round-2 LDS kernel
-    US = (-1, 1, 2, 4)
+    # interleaved A/B: -1 = point-lane form (r03), 0 = LDS records read one
+    # point ahead (r03), 1 / 2 / 4 = the round-2 LDS kernel
+    US = (-1, 0, 1, 2, 4)
     for rep in range(2):
         for u in US:
             L.acm_set_tuning(_lib.TUNE_FOV_UNROLL, u)
