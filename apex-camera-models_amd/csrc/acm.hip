@@ -2884,8 +2884,9 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid_rec(acm_camera cam, size
 // errors are summed lane-serially, then by the xor butterfly (the same bits
 // in every lane), and the finite count is a ballot popcount.  Lane l of a
 // wave keeps the running totals of grid values l, l + 64, ... in registers.
-// Every lane is busy (the grid-lane forms run 290 of 320 lanes) and the P
-// evaluations of a lane are independent chains.  The terms are those of the
+// Every lane is busy (the grid-lane forms run 290 of 320 lanes), the P
+// evaluations of a lane are independent chains, and NW grid values are
+// evaluated per step so that their butterflies' shuffles overlap.  The terms are those of the
 // forms above, bit for bit; only the summation order differs (the grid sums
 // are held to 1e-12 of the serial reference, counts exact).  Groups are split
 // evenly over all waves of a grid sized to the resident workgroups.
@@ -2893,9 +2894,11 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid_rec(acm_camera cam, size
 // 1 / (2 tan(w/2)) (2 per grid value; the host's IEEE divisions, the same
 // bits as the device's).
 constexpr int kFovPlBlock = 256;
-constexpr int kFovPlP = 3;
+// 3 points per lane, 2 grid values per step (5.36 ms on 9.3M correspondences;
+// P = 2 / 4 and 1 / 4 values per step 5.6-5.9 ms: profiles/r03fov_*.log)
+constexpr int kFovPlP = 3, kFovPlNW = 2;
 
-template <int LAYOUT, int P>
+template <int LAYOUT, int P, int NW>
 __global__ __launch_bounds__(kFovPlBlock) void k_fov_grid_pl(acm_camera cam, size_t n,
                                                              const double* __restrict__ pts,
                                                              const double* __restrict__ obs,
@@ -2947,67 +2950,89 @@ __global__ __launch_bounds__(kFovPlBlock) void k_fov_grid_pl(acm_camera cam, siz
                 gen = gen || (!small && !fast);
             }
         }
-        auto walk = [&](auto gen_c) {
+        // one grid value k: the wave's P x 64 errors summed lane-serially
+        // (s) and the finite count (c, wave-uniform)
+        auto eval_w = [&](auto gen_c, int k, double& s, uint32_t& c) {
             constexpr bool GEN = decltype(gen_c)::value;
+            const double w = table[3 * k], tw2 = table[3 * k + 1], rd0 = table[3 * k + 2];
+            const double iw = table[3 * kFovGrid + 2 * k];
+            const double itw2 = table[3 * kFovGrid + 2 * k + 1];
+            double d2[P], e[P];
+            bool slow = false;
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                // the evaluation of k_fov_grid, operand for operand
+                const double a = tw2 * rz[j];
+                const bool big = a > 1.0;
+                const double at = atan01(big ? itw2 * zr[j] : a);
+                const double atan_wrd = big ? 1.5707963267948966 - at : at;  // :196
+                const double rd = fma(rd0, fl[j], atan_wrd * ir[j] * iw);    // :205
+                const double du = fma(ax[j], rd, bx[j]), dv = fma(ay[j], rd, by[j]);
+                d2[j] = fma(du, du, dv * dv);
+                e[j] = d2[j] * rsq_nr(d2[j]);  // :211-213
+                slow = slow || !nr_range(d2[j]);
+            }
+            if (GEN) {
+#pragma unroll
+                for (int j = 0; j < P; ++j) {
+                    const size_t i = g * kGroup + (size_t)j * 64 + lane;
+                    if (i < n && fl[j] == 0.0 && ir[j] == 0.0) {
+                        double x, y, z;
+                        load_point<LAYOUT>(pts, n, i, x, y, z);
+                        const double r2 = x * x + y * y, rr = sqrt(r2);
+                        const double rdg = fov_rd_general(tw2, rr, z, w, r2, rd0);
+                        const double du = (fx * (x * rdg) + cx) - obs[2 * i];
+                        const double dv = (fy * (y * rdg) + cy) - obs[2 * i + 1];
+                        d2[j] = fma(du, du, dv * dv);
+                        e[j] = d2[j] * rsq_nr(d2[j]);
+                        slow = slow || !nr_range(d2[j]);
+                    }
+                }
+            }
+            if (slow) {  // 0, huge or NaN: the IEEE sqrt
+#pragma unroll
+                for (int j = 0; j < P; ++j)
+                    if (!nr_range(d2[j])) e[j] = sqrt(d2[j]);
+            }
+            s = 0.0;
+            c = 0;
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const bool f = isfinite(e[j]);
+                s += f ? e[j] : 0.0;
+                c += (uint32_t)__popcll(__ballot(f));
+            }
+        };
+        auto walk = [&](auto gen_c) {
 #pragma unroll
             for (int b = 0; b < kWB; ++b) {
                 const int wl_end = kFovGrid - b * 64 < 64 ? kFovGrid - b * 64 : 64;
-                for (int wl = 0; wl < wl_end; ++wl) {
-                    const int k = b * 64 + wl;
-                    const double w = table[3 * k], tw2 = table[3 * k + 1],
-                                 rd0 = table[3 * k + 2];
-                    const double iw = table[3 * kFovGrid + 2 * k];
-                    const double itw2 = table[3 * kFovGrid + 2 * k + 1];
-                    double d2[P], e[P];
-                    bool slow = false;
+                // NW grid values per step, their butterflies interleaved
+                static_assert(64 % NW == 0, "grid values in steps of NW");
+                for (int wl = 0; wl < wl_end; wl += NW) {
+                    double sv[NW];
+                    uint32_t cv[NW];
 #pragma unroll
-                    for (int j = 0; j < P; ++j) {
-                        // the evaluation of k_fov_grid, operand for operand
-                        const double a = tw2 * rz[j];
-                        const bool big = a > 1.0;
-                        const double at = atan01(big ? itw2 * zr[j] : a);
-                        const double atan_wrd = big ? 1.5707963267948966 - at : at;  // :196
-                        const double rd = fma(rd0, fl[j], atan_wrd * ir[j] * iw);    // :205
-                        const double du = fma(ax[j], rd, bx[j]), dv = fma(ay[j], rd, by[j]);
-                        d2[j] = fma(du, du, dv * dv);
-                        e[j] = d2[j] * rsq_nr(d2[j]);  // :211-213
-                        slow = slow || !nr_range(d2[j]);
+                    for (int v = 0; v < NW; ++v) {
+                        sv[v] = 0.0;
+                        cv[v] = 0;
+                        if (wl_end % NW == 0 || wl + v < wl_end)
+                            eval_w(gen_c, b * 64 + wl + v, sv[v], cv[v]);
                     }
-                    if (GEN) {
 #pragma unroll
-                        for (int j = 0; j < P; ++j) {
-                            const size_t i = g * kGroup + (size_t)j * 64 + lane;
-                            if (i < n && fl[j] == 0.0 && ir[j] == 0.0) {
-                                double x, y, z;
-                                load_point<LAYOUT>(pts, n, i, x, y, z);
-                                const double r2 = x * x + y * y, rr = sqrt(r2);
-                                const double rdg = fov_rd_general(tw2, rr, z, w, r2, rd0);
-                                const double du = (fx * (x * rdg) + cx) - obs[2 * i];
-                                const double dv = (fy * (y * rdg) + cy) - obs[2 * i + 1];
-                                d2[j] = fma(du, du, dv * dv);
-                                e[j] = d2[j] * rsq_nr(d2[j]);
-                                slow = slow || !nr_range(d2[j]);
-                            }
+                    for (int off = 32; off > 0; off >>= 1) {
+                        double t[NW];
+#pragma unroll
+                        for (int v = 0; v < NW; ++v) t[v] = __shfl_xor(sv[v], off, 64);
+#pragma unroll
+                        for (int v = 0; v < NW; ++v) sv[v] += t[v];
+                    }
+#pragma unroll
+                    for (int v = 0; v < NW; ++v)
+                        if (lane == wl + v) {
+                            acc[b] += sv[v];
+                            accn[b] += cv[v];
                         }
-                    }
-                    if (slow) {  // 0, huge or NaN: the IEEE sqrt
-#pragma unroll
-                        for (int j = 0; j < P; ++j)
-                            if (!nr_range(d2[j])) e[j] = sqrt(d2[j]);
-                    }
-                    double s = 0.0;
-                    uint32_t c = 0;
-#pragma unroll
-                    for (int j = 0; j < P; ++j) {
-                        const bool f = isfinite(e[j]);
-                        s += f ? e[j] : 0.0;
-                        c += (uint32_t)__popcll(__ballot(f));
-                    }
-                    s = wave_sum(s);
-                    if (lane == wl) {
-                        acc[b] += s;
-                        accn[b] += c;
-                    }
                 }
             }
         };
@@ -4214,7 +4239,8 @@ static size_t fov_blocks_rec(size_t n) {
 // the point-lane form: >= one group per wave
 static size_t fov_blocks_pl(size_t n) {
     static const int cap = fov_cap(
-        reinterpret_cast<const void*>(k_fov_grid_pl<ACM_LAYOUT_AOS, kFovPlP>), kFovPlBlock);
+        reinterpret_cast<const void*>(k_fov_grid_pl<ACM_LAYOUT_AOS, kFovPlP, kFovPlNW>),
+        kFovPlBlock);
     const size_t per_block = (size_t)kFovPlBlock * kFovPlP;
     size_t nb = (n + per_block - 1) / per_block;
     if (nb > (size_t)cap) nb = cap;
@@ -4268,8 +4294,8 @@ ACM_API int acm_fov_grid_errors(const acm_camera* cam, size_t n, const double* p
     auto go = [&](auto lay_c, auto u_c) {
         constexpr int LAY = decltype(lay_c)::value, U = decltype(u_c)::value;
         if (fu < 0) {  // point-lane form (default)
-            hipLaunchKernelGGL((k_fov_grid_pl<LAY, kFovPlP>), dim3(nb), dim3(kFovPlBlock), 0, s,
-                               *cam, n, points_3d, points_2d, table, parts);
+            hipLaunchKernelGGL((k_fov_grid_pl<LAY, kFovPlP, kFovPlNW>), dim3(nb),
+                               dim3(kFovPlBlock), 0, s, *cam, n, points_3d, points_2d, table, parts);
         } else if (fu == 0) {  // record form
             hipLaunchKernelGGL((k_fov_grid_rec<LAY>), dim3(nb), dim3(kFovBlock), 0, s, *cam, n,
                                chunk, points_3d, points_2d, table, parts);
