@@ -272,6 +272,25 @@ def test_fov_grid_errors_match_oracle(n):
         assert (np.argmin(avg) + 10) / 100.0 == bw
 
 
+def test_fov_grid_point_lane_at_scale_with_scattered_special_points():
+    """The point-lane form walks many 192-point groups per wave; groups that
+    hold a general-form point (z <= 0, NaN) take the slow walk and the others
+    the branch-free one.  300K points with special points scattered over the
+    whole range (and a ragged tail): counts exact, sums within 1e-12 of the
+    serial oracle, the oracle's w chosen."""
+    p, xyz, uv = _fov_data(300_001, 17, noise=0.4)
+    rng = np.random.default_rng(5)
+    for k, idx in enumerate(rng.choice(xyz.shape[0], size=60, replace=False)):
+        xyz[idx] = [[0.0, 0.0, 1.0], [0.3, -0.2, 0.0], [np.nan, 0.1, 1.0], [1e-9, 0.0, 2.0],
+                    [0.2, 0.1, -1.0], [np.inf, 0.0, 1.0]][k % 6]
+    bw, s_ref, c_ref = O.fov_grid_search(p, xyz, uv)
+    s, c = _fov_grid_gpu(p, xyz, uv)
+    assert np.array_equal(c, c_ref)
+    assert np.all(np.abs(s - s_ref) <= 1e-12 * np.abs(s_ref) + 1e-300)
+    avg = np.where(c > 0, s / np.maximum(c, 1), np.inf)
+    assert (np.argmin(avg) + 10) / 100.0 == bw
+
+
 @pytest.mark.parametrize("n", [1, 7, 320 * 3 + 5, 20_001])
 def test_fov_grid_kernels_bit_identical(n):
     """The record form of the grid search (0) and the round-2 LDS form (1, 2,
