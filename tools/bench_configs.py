@@ -28,10 +28,17 @@ def timed(fn, reps=20, warm=3, blocks=3):
     ctypes/Python cost of each call overlaps the previous call's kernels
     instead of being counted as GPU time; the fastest block is the steady
     state, free of clock ramps and other processes' interference)."""
+    import time
+
     import torch
-    for _ in range(warm):
-        fn()
+    # at least `warm` calls and >= 50 ms of them: the clocks ramp over
+    # milliseconds (a few calls of a 0.08 ms kernel timed it ~10% slow)
     torch.cuda.synchronize()
+    t0, k = time.perf_counter(), 0
+    while k < warm or time.perf_counter() - t0 < 0.05:
+        fn()
+        torch.cuda.synchronize()
+        k += 1
     best = float("inf")
     for _ in range(blocks):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
