@@ -59,6 +59,14 @@ def parse():
     ap.add_argument("--no-jacobian", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--legs", default="4,5",
+                    help="BASELINE configs measured after the headline's timed region and "
+                         "attached as sub-objects (config4 / config5); 'none' to skip")
+    ap.add_argument("--leg4-points", type=int, default=50_000_000,
+                    help="config 4: points in total over all ranks (strong scaling)")
+    ap.add_argument("--leg5-cells", type=int, default=100_000_000,
+                    help="config 5: requested sample_points cells in total")
+    ap.add_argument("--leg-steps", type=int, default=10)
     return ap.parse_args()
 
 
@@ -234,32 +242,262 @@ def launch_ranks(n):
     import signal
     import subprocess
     port = os.environ.get("MASTER_PORT") or str(_free_port())
+
+    def die_with_parent():
+        # runs in the child between fork and exec (the parent has touched no
+        # GPU): PR_SET_PDEATHSIG, so a parent killed outright (SIGKILL from
+        # `timeout -k`) still takes its ranks with it
+        try:
+            ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except Exception:
+            pass
+
+    class _Stop(Exception):
+        pass
+
+    def on_signal(signum, _frame):
+        raise _Stop(signum)
+
+    def signal_all(procs_, sig):
+        for q in procs_:
+            try:
+                os.killpg(q.pid, sig)
+            except (ProcessLookupError, PermissionError):
+                pass
+
+    # a SIGTERM / SIGINT / SIGHUP to the parent (Ctrl-C, a timeout that
+    # signals only the parent's group) is forwarded to every rank's own
+    # process group below instead of leaving the ranks orphaned
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)}
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
-                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
-                                      env=env, start_new_session=True))
+    live = []
     rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 1
-                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the "
-                      f"other ranks", file=sys.stderr, flush=True)
-                for q in live:
-                    try:
-                        os.killpg(q.pid, signal.SIGTERM)
-                    except ProcessLookupError:
-                        pass
-        time.sleep(0.05)
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                       MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+            p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                 env=env, start_new_session=True, preexec_fn=die_with_parent)
+            procs.append(p)
+            live.append(p)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the "
+                          f"other ranks", file=sys.stderr, flush=True)
+                    signal_all(live, signal.SIGTERM)
+            time.sleep(0.05)
+    except _Stop as e:
+        sig = e.args[0]
+        print(f"bench.py: received signal {sig}; stopping the ranks", file=sys.stderr, flush=True)
+        rc = 128 + sig
+    finally:
+        # whatever ended the loop, no rank outlives the parent: SIGTERM to
+        # each rank's process group, SIGKILL after a 5 s grace period
+        live = [p for p in procs if p.poll() is None]
+        if live:
+            signal_all(live, signal.SIGTERM)
+            t_end = time.time() + 5.0
+            while time.time() < t_end and any(p.poll() is None for p in live):
+                time.sleep(0.05)
+            signal_all([p for p in live if p.poll() is None], signal.SIGKILL)
+            for p in live:
+                try:
+                    p.wait(timeout=5)
+                except subprocess.TimeoutExpired:
+                    pass
+        for s, h in old.items():
+            signal.signal(s, h)
     return rc
+
+
+class LegCtx:
+    """What the BASELINE config-4/5 legs need of the run: rank, world, the
+    process group (None at N = 1) and the device of the collectives'
+    tensors (the GPU under RCCL, the CPU under the gloo rehearsal)."""
+
+    def __init__(self, rank, world, dist, cdev):
+        self.rank, self.world, self.dist, self.cdev = rank, world, dist, cdev
+
+    def sync(self):
+        import torch
+        if self.dist:
+            self.dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(self, v):
+        import torch
+        if not self.dist:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.cdev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t[0])
+
+
+LEG4_MODELS = {0: "pinhole", 1: "rad_tan", 2: "kannala_brandt", 3: "double_sphere", 4: "ucm",
+               5: "eucm"}
+
+
+def leg_config4(ctx, n_total, reps):
+    """BASELINE config 4: all six models, project -> unproject round trip over
+    `n_total` points in total (strong scaling: contiguous shards of one global
+    batch), then ONE all-reduce of every model's (sum of squared round-trip
+    errors, round-trip-ok count) -- the residual all-reduce of the config.
+    A step = the six round trips (12 launches, uv intermediate in HBM); the
+    error reduction runs after the timed steps, the all-reduce is timed on its
+    own.  The reference loop this batches: project then unproject per point
+    for every model (tests/projection_accuracy.rs, mod.rs:256/271)."""
+    import torch
+    from apex_camera_models import _lib, samples
+    from apex_camera_models.camera import MODEL_CLASSES, Resolution
+    from apex_camera_models.distributed import shard_range
+    lo, hi = shard_range(n_total, ctx.rank, ctx.world)
+    n = hi - lo
+    dev = torch.device("cuda", torch.cuda.current_device())
+    L = _lib.load()
+    sh = torch.cuda.current_stream().cuda_stream
+    pts = samples.synthetic_points_device(n, offset=lo)
+    uv = torch.empty((max(n, 1), 2), dtype=torch.float64, device=dev)
+    cams, outs = [], []
+    for mid, name in LEG4_MODELS.items():
+        params, (w, h) = samples.SAMPLES[mid]
+        cams.append(MODEL_CLASSES[name]._from_params(params, Resolution(w, h)).acm_camera())
+        outs.append((torch.empty((max(n, 1),), dtype=torch.uint8, device=dev),
+                     torch.empty((max(n, 1), 3), dtype=torch.float64, device=dev),
+                     torch.empty((max(n, 1),), dtype=torch.uint8, device=dev)))
+
+    def one(k):
+        cam, (st, ray, st2) = cams[k], outs[k]
+        rc = L.acm_project(ctypes.byref(cam), n, pts.data_ptr(), 0, uv.data_ptr(), st.data_ptr(),
+                           None, sh)
+        rc = rc or L.acm_unproject(ctypes.byref(cam), n, uv.data_ptr(), ray.data_ptr(), 0,
+                                   st2.data_ptr(), sh)
+        if rc:
+            _lib.check(rc)
+
+    def step():
+        for k in range(len(cams)):
+            one(k)
+
+    step()
+    ctx.sync()
+    per_model = []
+    for k in range(len(cams)):  # each model's round trip on its own
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            one(k)
+        ctx.sync()
+        per_model.append(ctx.max_over_ranks((time.perf_counter() - t0) / reps * 1e3))
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    ctx.sync()
+    ms = ctx.max_over_ranks((time.perf_counter() - t0) / reps * 1e3)
+    # round-trip residuals: ||ray - p / |p|||^2 over the points whose
+    # projection and unprojection are both Ok
+    finite = torch.isfinite(pts).all(1)
+    pn = pts / torch.linalg.norm(pts, dim=1, keepdim=True)
+    red = torch.empty((2 * len(cams),), dtype=torch.float64, device=dev)
+    for k, (st, ray, st2) in enumerate(outs):
+        ok = (st[:n] == 0) & (st2[:n] == 0) & finite
+        e2 = ((ray[:n] - pn) ** 2).sum(1)
+        red[2 * k] = torch.where(ok, e2, torch.zeros_like(e2)).sum()
+        red[2 * k + 1] = ok.sum().to(torch.float64)
+    vec = red.to(ctx.cdev)
+    coll_us = None
+    if ctx.dist:
+        tot = vec.clone()
+        ctx.dist.all_reduce(tot)
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            tot.copy_(vec)
+            ctx.dist.all_reduce(tot)
+        ctx.sync()
+        coll_us = ctx.max_over_ranks((time.perf_counter() - t0) / reps * 1e6)
+        vec = tot
+    vec = vec.cpu().tolist()
+    models = {}
+    for k, name in enumerate(LEG4_MODELS.values()):
+        models[name] = {"round_trip_ms": round(per_model[k], 4),
+                        "Mpoints_per_s": round(n_total / per_model[k] / 1e3, 1),
+                        "round_trip_ok": int(vec[2 * k + 1]),
+                        "rms_round_trip_err": (vec[2 * k] / vec[2 * k + 1]) ** 0.5
+                        if vec[2 * k + 1] else None}
+    del pts, uv, outs, pn
+    torch.cuda.empty_cache()
+    return {"what": "6 models x project->unproject round trip (strong: one global batch "
+                    "sharded over the ranks) + all-reduce of (sum err^2, n_ok) per model",
+            "points_total": n_total, "points_per_rank": n, "steps": reps,
+            "ms_per_step": round(ms, 4),
+            "value": round(len(cams) * n_total / ms / 1e3, 1),
+            "unit": "Mround-trips/s (all 6 models, whole job)",
+            "scaling": "strong", "allreduce_us": None if coll_us is None else round(coll_us, 2),
+            "models": models}
+
+
+def leg_config5(ctx, n_cells):
+    """BASELINE config 5: KB -> DS conversion on ~`n_cells` sampled
+    correspondences (camera_converter.rs:355-488: sample_points, linear
+    estimation, bounded LM, reprojection errors).  Grid rows of sample_points
+    are sharded over the ranks (each keeps its own correspondences, no data
+    exchange), and the conversion runs over the union: merged TSQR factors,
+    one all-reduce of the normal equations per LM evaluation, merged
+    statistics and the distributed exact median (distributed.py)."""
+    import torch
+    from apex_camera_models import KannalaBrandtModel, Resolution, conversion, samples
+    from apex_camera_models import distributed as D
+    kp, (w, h) = samples.SAMPLES[2]
+    src = KannalaBrandtModel._from_params(kp, Resolution(w, h))
+    from apex_camera_models import _lib
+    fn = D.gpu_sample_points_range(src, n_cells)
+    gx, gy = ctypes.c_uint32(), ctypes.c_uint32()  # the grid acm_sample_points uses
+    _lib.check(_lib.load().acm_sample_points_grid(w, h, n_cells, ctypes.byref(gx),
+                                                  ctypes.byref(gy)))
+    ncx, ncy = gx.value, gy.value
+
+    def sample():
+        if ctx.dist:
+            uv, xyz, _, total = D.sharded_sample_points(ncx, ncy, ctx.rank, ctx.world, fn)
+        else:
+            uv, xyz = fn(0, ncx * ncy)
+            total = int(uv.shape[0])
+        return uv, xyz, total
+
+    uv, xyz, _ = sample()  # warm-up: the caching allocator's first multi-GB blocks
+    del uv, xyz
+    ctx.sync()
+    t0 = time.perf_counter()
+    uv, xyz, total = sample()
+    ctx.sync()
+    t_s = ctx.max_over_ranks(time.perf_counter() - t0)
+    allreduce = D.rccl_allreduce() if ctx.dist else None
+    ctx.sync()
+    t0 = time.perf_counter()
+    met = conversion.convert(src, "double_sphere", xyz, uv, allreduce=allreduce)
+    ctx.sync()
+    t_c = ctx.max_over_ranks(time.perf_counter() - t0)
+    out = {"what": "KB->DS conversion: sharded sample_points + linear estimation + bounded LM "
+                   "+ reprojection errors",
+           "requested_cells": n_cells, "grid": [ncx, ncy], "correspondences_total": total,
+           "correspondences_rank0": int(uv.shape[0]), "sample_points_ms": round(t_s * 1e3, 3),
+           "convert_ms": round(t_c * 1e3, 3),
+           "optimization_ms_rank0": round(met.optimization_time_ms, 3),
+           "lm_iterations": met.lm_iterations, "termination": met.lm_termination,
+           "final_mean_px": met.final_reprojection_error.mean,
+           "final_median_px": met.final_reprojection_error.median,
+           "ds_params": met.model.params(), "scaling": "strong"}
+    del uv, xyz
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -458,6 +696,19 @@ def main():
     coll["global_n_valid"] = int(red[1])
     coll["global_rmse_px"] = (float(red[0]) / float(red[1])) ** 0.5 if float(red[1]) else None
 
+    # BASELINE configs 4 and 5 (the multi-GPU configs), after the headline's
+    # timed region and its collective: sub-objects of the one line
+    legs = {}
+    want_legs = set() if a.legs == "none" else set(a.legs.split(","))
+    if want_legs:
+        del pts, obs, sto, pts_aos
+        torch.cuda.empty_cache()
+        ctx = LegCtx(rank, world, dist if world > 1 else None, cdev)
+        if "4" in want_legs:
+            legs["config4"] = leg_config4(ctx, a.leg4_points, a.leg_steps)
+        if "5" in want_legs:
+            legs["config5"] = leg_config5(ctx, a.leg5_cells)
+
     if rank == 0:
         bpp = 24 + 16 + 1 + (16 * P if want_j else 0)
         kern_ms = main_res["kernel_ms"]
@@ -499,6 +750,7 @@ def main():
             out["shards_match_single_projection"] = main_res["shards_match_single_projection"]
         if other is not None:
             out[other["mode"]] = other
+        out.update(legs)
         if not a.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             out["cpu_baseline"] = cpu_baseline(model_id, params, w, h, main_res["points_per_rank"],
                                                a.cpu_baseline_seconds)

@@ -67,6 +67,23 @@ def main():
         if "SQ_ACTIVE_INST_VALU" in med and med.get("GRBM_GUI_ACTIVE"):
             row["valu_busy"] = med["SQ_ACTIVE_INST_VALU"] * 4 / (
                 SIMDS * med["GRBM_GUI_ACTIVE"] / 8)
+        # per-CU unit busy / stall shares (TA, TD, TCP: one instance per CU,
+        # 256 CUs, summed over instances; GRBM_GUI_ACTIVE summed over 8 XCDs)
+        if med.get("GRBM_GUI_ACTIVE"):
+            cyc = 256 * med["GRBM_GUI_ACTIVE"] / 8
+            for cn, key in (("TA_TA_BUSY_sum", "ta_busy"),
+                            ("TA_ADDR_STALLED_BY_TC_CYCLES_sum", "ta_addr_stalled_by_tc"),
+                            ("TD_TD_BUSY_sum", "td_busy"), ("TD_TC_STALL_sum", "td_tc_stall"),
+                            ("TCP_PENDING_STALL_CYCLES_sum", "tcp_pending_stall"),
+                            ("TCP_TCR_TCP_STALL_CYCLES_sum", "tcp_tcr_stall")):
+                if cn in med:
+                    row[key] = med[cn] / cyc
+        if med.get("SQ_WAVE_CYCLES"):
+            for cn, key in (("SQ_WAIT_ANY", "wait_any_share"),
+                            ("SQ_WAIT_INST_ANY", "wait_inst_share"),
+                            ("SQ_ACTIVE_INST_ANY", "active_inst_share")):
+                if cn in med:
+                    row[key] = med[cn] / med["SQ_WAVE_CYCLES"]
         if "SQ_INSTS_VALU" in med and med.get("SQ_WAVES"):
             row["valu_insts_per_wave"] = med["SQ_INSTS_VALU"] / med["SQ_WAVES"]
         if "SQ_INSTS_VALU_FLOPS_FP64" in med and us:
@@ -80,14 +97,18 @@ def main():
             row["hbm_frac_of_peak"] = row["hbm_GBps"] / HBM_PEAK_GBS
         out[k] = row
     json.dump(out, open(a.out, "w"), indent=1)
-    print(f"| kernel | avg us | VALU busy | VALU inst/wave | FP64 TF (frac) | HBM GB/s (frac) |")
-    print("|---|---|---|---|---|---|")
+    print(f"| kernel | avg us | VALU busy | VALU inst/wave | FP64 TF (frac) | HBM GB/s (frac) "
+          f"| TA busy | TD busy | wait / issue-stall / active |")
+    print("|---|---|---|---|---|---|---|---|---|")
     for k, r in sorted(out.items(), key=lambda kv: -kv[1].get("avg_us", 0)):
         f = lambda x, fmt: (fmt % x) if x is not None else "-"  # noqa: E731
         print(f"| {k} | {f(r.get('avg_us'), '%.1f')} | {f(r.get('valu_busy'), '%.2f')} | "
               f"{f(r.get('valu_insts_per_wave'), '%.0f')} | "
               f"{f(r.get('fp64_tflops'), '%.1f')} ({f(r.get('fp64_frac_of_peak'), '%.2f')}) | "
-              f"{f(r.get('hbm_GBps'), '%.0f')} ({f(r.get('hbm_frac_of_peak'), '%.2f')}) |")
+              f"{f(r.get('hbm_GBps'), '%.0f')} ({f(r.get('hbm_frac_of_peak'), '%.2f')}) | "
+              f"{f(r.get('ta_busy'), '%.2f')} | {f(r.get('td_busy'), '%.2f')} | "
+              f"{f(r.get('wait_any_share'), '%.2f')} / {f(r.get('wait_inst_share'), '%.2f')} / "
+              f"{f(r.get('active_inst_share'), '%.2f')} |")
 
 
 if __name__ == "__main__":

@@ -73,3 +73,72 @@ def test_self_launch_failing_ranks_exit_nonzero():
                        timeout=300)
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def _start_parent(tmp_path):
+    """A launch_ranks parent (bench.launch_ranks(2)) whose ranks are stand-ins
+    that record their pid and sleep; returns (parent Popen, rank pids)."""
+    import time
+    rec = tmp_path / "pids"
+    rec.mkdir()
+    child = tmp_path / "child.py"
+    child.write_text(
+        "import os, time\n"
+        f"open(os.path.join({str(rec)!r}, os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+        "time.sleep(600)\n")
+    parent = tmp_path / "parent.py"
+    parent.write_text(
+        "import sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import bench\n"
+        f"bench.__file__ = {str(child)!r}\n"
+        "sys.argv = ['bench.py', '--gpus', '2']\n"
+        "sys.exit(bench.launch_ranks(2))\n")
+    p = subprocess.Popen([sys.executable, str(parent)], env=_env(), stderr=subprocess.PIPE,
+                         text=True)
+    t_end = time.time() + 60
+    while time.time() < t_end and len(list(rec.iterdir())) < 2:
+        time.sleep(0.05)
+    time.sleep(0.2)
+    pids = [int((rec / str(r)).read_text()) for r in range(2)]
+    return p, pids
+
+
+def _gone(pids, timeout=15.0):
+    import time
+    t_end = time.time() + timeout
+    while time.time() < t_end:
+        alive = []
+        for pid in pids:
+            try:
+                os.kill(pid, 0)
+                # a zombie awaiting its (dead) parent's reaping is gone too
+                with open(f"/proc/{pid}/stat") as f:
+                    if f.read().split(")")[-1].split()[0] != "Z":
+                        alive.append(pid)
+            except (ProcessLookupError, FileNotFoundError):
+                pass
+        if not alive:
+            return True
+        time.sleep(0.1)
+    return False
+
+
+def test_parent_sigterm_stops_ranks(tmp_path):
+    """a SIGTERM to the parent (which started its ranks in their
+    own sessions) is forwarded to every rank; the parent exits 128 + 15"""
+    import signal
+    p, pids = _start_parent(tmp_path)
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    assert _gone(pids), pids
+
+
+def test_parent_sigkill_stops_ranks(tmp_path):
+    """a parent killed outright (timeout -k's SIGKILL) still takes its ranks
+    with it (PR_SET_PDEATHSIG in each rank)"""
+    import signal
+    p, pids = _start_parent(tmp_path)
+    p.send_signal(signal.SIGKILL)
+    p.wait(timeout=30)
+    assert _gone(pids), pids

@@ -39,6 +39,9 @@ def test_bench_single_gpu_line():
     assert d["value"] > 0 and 0 < d["roofline"]["frac"] < 1.0
     assert d["collective"]["global_n_valid"] > 0.99 * 300000
     assert "traffic_source" in d["roofline"]
+    assert d["config4"]["points_total"] == 50_000_000 and d["config4"]["value"] > 0
+    assert d["config5"]["correspondences_total"] == 92_935_075
+    assert d["config5"]["final_mean_px"] < 0.01
 
 
 def test_bench_self_launch_world2():
@@ -49,7 +52,8 @@ def test_bench_self_launch_world2():
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
                         "--steps", "3", "--warmup", "1", "--points", "300000",
-                        "--no-cpu-baseline"],
+                        "--no-cpu-baseline", "--leg4-points", "600001",
+                        "--leg5-cells", "2000000", "--leg-steps", "2"],
                        capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     d = _line(r.stdout)
@@ -57,6 +61,25 @@ def test_bench_self_launch_world2():
     assert d["config"]["global_points"] == 600000
     assert d["strong"]["mode"] == "strong" and d["strong"]["global_points"] == 300000
     assert d["collective"]["ranks"] == 2 and d["collective"]["us"] > 0
+    # BASELINE config 4 over both ranks: the all-reduced counts equal the
+    # single-process leg's (same global batch, sharded)
+    c4 = d["config4"]
+    assert c4["points_total"] == 600001 and c4["points_per_rank"] == 300001
+    assert c4["allreduce_us"] > 0 and c4["value"] > 0 and len(c4["models"]) == 6
+    one = _line(subprocess.run(
+        [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0",
+         "--points", "1000", "--no-cpu-baseline", "--legs", "4", "--leg4-points", "600001",
+         "--leg-steps", "1"], capture_output=True, text=True, timeout=300, cwd=ROOT).stdout)
+    for name, m in c4["models"].items():
+        m1 = one["config4"]["models"][name]
+        assert m["round_trip_ok"] == m1["round_trip_ok"] > 0.8 * 600001, name
+        assert abs(m["rms_round_trip_err"] - m1["rms_round_trip_err"]) <= \
+            1e-9 * m1["rms_round_trip_err"] + 1e-300, name
+    # BASELINE config 5: row-sharded sample_points + the sharded conversion
+    c5 = d["config5"]
+    assert c5["correspondences_total"] > c5["correspondences_rank0"] > 0
+    assert c5["final_mean_px"] < 0.05 and c5["lm_iterations"] > 0
+    assert c5["convert_ms"] > 0 and c5["sample_points_ms"] > 0
 
 
 def test_bench_world2_strong_rehearsal():

@@ -121,7 +121,8 @@ def test_config5_kb_to_ds_on_92_9m_correspondences():
     (camera_converter.rs:355-488: linear estimation + bounded LM, all on the
     GPU).  At the final parameters the fused normal equations over all
     92.9M points have the oracle's n_valid exactly, and on a strided 1M
-    subsample the GPU's JtJ / Jtr / cost equal the oracle's within 1e-10."""
+    subsample the GPU's JtJ / Jtr / cost equal the oracle's within 1e-10.
+    Then the config's f32-vs-f64 sweep over all 92.9M points."""
     import torch
     from apex_camera_models import conversion, factors, util
     from apex_camera_models.camera import Resolution
@@ -149,3 +150,16 @@ def test_config5_kb_to_ds_on_92_9m_correspondences():
     ref = np.concatenate([JtJ.ravel(), Jtr, [cost]])
     scale = np.maximum(np.abs(ref), np.abs(ref).max() * 1e-6)
     assert (np.abs(got[:-1] - ref) / scale).max() <= 1e-10
+    # BASELINE config 5's f32-vs-f64 tolerance sweep at scale: the DS
+    # projection at the optimum over all 92.9M correspondences in f32
+    # (acm_project_f32) agrees with the f64 path on every status, and its
+    # pixels are within 1e-4 relative (floor 1 px; measured 7.5e-5)
+    ds = met.model
+    uv64, st64, _ = ds.project_batch(xyz)
+    uv32, st32, _ = ds.project_batch(xyz.to(torch.float32))
+    assert uv32.dtype == torch.float32
+    assert int((st64 != st32).sum()) == 0
+    both = (st64 == 0) & (st32 == 0)
+    d = ((uv32.double() - uv64).abs() / uv64.abs().clamp(min=1.0)).max(dim=1).values
+    worst = float(torch.where(both, d, torch.zeros_like(d)).max())
+    assert 0.0 < worst < 1e-4, worst
