@@ -172,6 +172,7 @@ __device__ __forceinline__ Cam<T> make_cam(const acm_camera& c) {
     k.kc[0] = T(INFINITY);  // no certified interval (sample_points only)
 #pragma unroll
     for (int i = 0; i < 2 * kRayPolyN; ++i) k.rp[i] = T(0);
+    k.rpl = nullptr;
     return k;
 }
 
@@ -193,7 +194,24 @@ __device__ __forceinline__ Cam<T> make_cam(const CamArg& c) {
     for (int i = 0; i < 12; ++i) k.kc[i] = c.kc[i];
 #pragma unroll
     for (int i = 0; i < 2 * kRayPolyN; ++i) k.rp[i] = c.rp[i];
+    k.rpl = nullptr;
     return k;
+}
+
+// The sample_points kernels' camera: make_cam, plus (TagKbPoly) the ray
+// polynomials staged in LDS as (C_i, S_i) pairs for ray_certified<true>.
+// Every thread of the workgroup must call it (it synchronises).
+template <class TagT>
+__device__ __forceinline__ Cam<double> sample_cam(const CamArg& cam) {
+    Cam<double> c = make_cam<double>(cam);
+    if constexpr (SampleTag<TagT>::poly) {
+        __shared__ RayPolyPair s_rp[kRayPolyN];
+        if (threadIdx.x < kRayPolyN)
+            s_rp[threadIdx.x] = RayPolyPair{cam.rp[threadIdx.x], cam.rp[kRayPolyN + threadIdx.x]};
+        __syncthreads();
+        c.rpl = (lds_ray_poly*)s_rp;
+    }
+    return c;
 }
 
 // NTL: non-temporal loads (read-once streams; the read probe measured 6.9 vs
@@ -282,9 +300,11 @@ static std::atomic<int> g_nt_loads_unproject{-1};
 // per-point LDS record form, 1 / 2 / 4 = the LDS form with that many points
 // per lane step.
 static std::atomic<int> g_fov_unroll{-1};
-// sample_points: -1 = auto = single pass with decoupled look-back and the
-// per-model tile (SampleR), 0 = the two-pass count / scan / write path,
-// 1 / 2 / 3 = single pass with tiles of 4 / 8 / 16 x 256 cells.
+// sample_points (include/acm.h ACM_TUNE_SAMPLE_FUSED): -1 = auto = the
+// segment two-pass path (certified counts, scan, write) -- the speculative
+// segment path (4) for RadTan; 0 = the round-1 two-pass count / scan /
+// write path; 1 / 2 / 3 = single pass with a decoupled look-back, tiles of
+// 2 / 4 / 8 x 256 cells; 4 = speculative segments.
 static std::atomic<int> g_sample_fused{-1};
 // sample_points look-back: polls of an unpublished predecessor's status word
 // before the waiting wave counts that tile's cells itself (-1 = auto =
@@ -1404,7 +1424,7 @@ constexpr size_t kSampleCells = (size_t)kBlock * kSampleR;
 template <class TagT>
 __global__ __launch_bounds__(kBlock) void k_sample_count(CamArg cam, Grid g, size_t cells,
                                                          uint64_t* __restrict__ counts) {
-    const Cam<double> c = make_cam<double>(cam);
+    const Cam<double> c = sample_cam<TagT>(cam);
     const size_t base = (size_t)blockIdx.x * kSampleCells;
     uint32_t mine = 0;
     CellWalk cw;
@@ -1465,7 +1485,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_write(CamArg cam, Grid g, siz
                                                          const uint64_t* __restrict__ offsets,
                                                          double* __restrict__ uv_out,
                                                          double* __restrict__ xyz_out) {
-    const Cam<double> c = make_cam<double>(cam);
+    const Cam<double> c = sample_cam<TagT>(cam);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     __shared__ uint32_t sm[kBlock / 64];
     const size_t base = (size_t)blockIdx.x * kSampleCells;
@@ -1798,7 +1818,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(CamArg cam, Grid g, size_t
         // segments' speculative offsets are right up to its first partial one
         // -- the scan below decides per segment
     }
-    const Cam<double> c = make_cam<double>(cam);
+    const Cam<double> c = sample_cam<TagT>(cam);
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nseg = (cells + kSegCells - 1) / kSegCells;
@@ -1899,7 +1919,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_spec(CamArg cam, Grid g, size_t 
     // one workgroup per count block (256 segments), wave w takes segments
     // w, w + 4, ... so the four waves write adjacent runs at the same time
     constexpr int SPW = kSegPerBlock / 4;
-    const Cam<double> c = make_cam<double>(cam);
+    const Cam<double> c = sample_cam<TagT>(cam);
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nseg = (cells + kSegCells - 1) / kSegCells;
@@ -1992,7 +2012,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kFusedR 
                                                          double* __restrict__ uv_out,
                                                          double* __restrict__ xyz_out,
                                                          uint64_t* __restrict__ out_counts) {
-    const Cam<double> c = make_cam<double>(cam);
+    const Cam<double> c = sample_cam<TagT>(cam);
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     __shared__ uint64_t s_excl;
@@ -4483,12 +4503,21 @@ ACM_API const char* acm_last_error(void) { return g_last_error.c_str(); }
 // The version string names the compile-time variant of the build (the
 // diagnostic / A-B defines), so a counter file collected on one variant
 // cannot be attributed to another (bench.py load_traffic).
-ACM_API const char* acm_version(void) {
-    return "acm 0.3.0 (gfx950"
-#ifdef ACM_IEEE_MATH
-           "; ACM_IEEE_MATH"
+// ACM_BUILD_DEFINES: the Makefile passes every extra define of an A/B or
+// diagnostic build (AB=..., HIPFLAGS additions) as a string, so the version
+// names them whatever the library file is called.
+#ifndef ACM_BUILD_DEFINES
+#define ACM_BUILD_DEFINES ""
 #endif
-           ")";
+ACM_API const char* acm_version(void) {
+    static const std::string v = std::string("acm 0.4.0 (gfx950") +
+#ifdef ACM_IEEE_MATH
+                                 "; ACM_IEEE_MATH" +
+#endif
+                                 (ACM_BUILD_DEFINES[0] ? std::string("; ") + ACM_BUILD_DEFINES
+                                                       : std::string()) +
+                                 ")";
+    return v.c_str();
 }
 
 }  // extern "C"

@@ -27,7 +27,7 @@
 //     reference's loop, certified per step against an error bound; any
 //     pixel that cannot be certified runs the reference's loop from the
 //     start.  Statuses are the reference's; rays within a few ulp.
-//     ACM_TUNE_NEWTON_FAST = 0 runs the reference's loops for every pixel
+//     ACM_REFERENCE_NEWTON (per call) runs the reference's loops for every pixel
 //     (RadTan's rays are then the reference's bit for bit).
 //   * FOV project: atan2 is atan2_ge0; FOV unproject: sincos_0_2 and
 //     rsq / rcp + Newton for 1 / rd, 1 / cos and 1 / |p| (its one decision,
@@ -283,6 +283,12 @@ __device__ __forceinline__ bool norm_below_1e6(T sq) {
 
 // Coefficients of each of KB's certified-ray polynomials (degree 16 in r2)
 constexpr int kRayPolyN = 17;
+// One Horner step's coefficients of both ray polynomials, (C_i, S_i), as the
+// sample_points kernels stage them in LDS (acm.hip poly_to_lds).
+struct alignas(16) RayPolyPair {
+    double c, s;
+};
+typedef __attribute__((address_space(3))) const RayPolyPair lds_ray_poly;
 
 // Uniform camera parameters, converted once per thread from the kernel
 // argument (they stay in SGPRs: every lane reads the same values).
@@ -304,6 +310,12 @@ struct Cam {
     // (cos theta*, sin theta* / ru in r2; acm.hip kb_fit_ray).
     T kc[12];
     T rp[2 * kRayPolyN];
+    // The same polynomials staged in LDS by the sample_points kernels (r04):
+    // ray_certified<true> reads them from there, per evaluation, instead of
+    // holding 34 doubles in SGPRs across the kernel -- together with the
+    // general path's constants they exceeded the 102 SGPRs and spilled to
+    // VGPR lanes (~100 v_readlane per 64-cell segment on the hot path).
+    lds_ray_poly* rpl;
 };
 
 // (u - cx) / fx with fx uniform: RN(a / b) from the host's RN(1 / b) and the
@@ -558,7 +570,7 @@ struct RadTan {
         }
 #ifndef ACM_IEEE_MATH
         if constexpr (sizeof(T) == 8) {
-            T px, py;  // uk[0] NaN: unbounded terms, or ACM_TUNE_NEWTON_FAST = 0
+            T px, py;  // uk[0] NaN: unbounded terms, or ACM_REFERENCE_NEWTON
             if (c.uk[0] == c.uk[0] && newton_fast(c, s.tx, s.ty, px, py)) {
                 // (x, y, 1).normalize() with 1 / |p| from rsq + Newton (~1 ulp)
                 const T in = rsq_nr(fma(px, px, fma(py, py, T(1))));
@@ -760,7 +772,7 @@ struct KannalaBrandt {
     // success ir ~= 1 / ru (the rsq itself, or 2 / pi after the clamp).
     __device__ static __forceinline__ bool front_fast(const Cam<T>& c, T r2, T& ru, T& theta,
                                                       T& ir) {
-        // uk[0] NaN: the camera's terms are unbounded, or ACM_TUNE_NEWTON_FAST = 0
+        // uk[0] NaN: the camera's terms are unbounded, or ACM_REFERENCE_NEWTON
         if (!nr_range(r2) || !(c.uk[0] == c.uk[0])) return false;
         const T y = rsq_nr(r2);
         const T rf = r2 * y;
@@ -799,11 +811,17 @@ struct KannalaBrandt {
     __device__ static __forceinline__ void ray_certified(const Cam<T>& c, T mx, T my, T r2, T& X,
                                                          T& Y, T& Z) {
         if constexpr (POLY) {
-            T cp = c.rp[kRayPolyN - 1], sp = c.rp[2 * kRayPolyN - 1];
+            // (C_i, S_i) pairs from LDS, one ds_read_b128 broadcast each; the
+            // empty asm makes the table address opaque per evaluation, so
+            // the reads stay here instead of being hoisted out of the
+            // kernel's loops into 68 registers
+            lds_ray_poly* q = c.rpl;
+            asm volatile("" : "+v"(q));
+            T cp = q[kRayPolyN - 1].c, sp = q[kRayPolyN - 1].s;
 #pragma unroll
             for (int i = kRayPolyN - 2; i >= 0; --i) {
-                cp = fma(cp, r2, c.rp[i]);
-                sp = fma(sp, r2, c.rp[kRayPolyN + i]);
+                cp = fma(cp, r2, q[i].c);
+                sp = fma(sp, r2, q[i].s);
             }
             X = mx * sp;
             Y = my * sp;
@@ -1200,8 +1218,8 @@ struct Fov {
         T my = div_by_f(v - cy, fy, c.ify);
 #ifndef ACM_IEEE_MATH
         if constexpr (sizeof(T) == 8) {
-            // Values-only fast form (uk[0] == 1; ACM_TUNE_NEWTON_FAST = 0 sets
-            // NaN): rd and 1 / rd from rsq, sin / cos of rd w by sincos_0_2,
+            // Values-only fast form (uk[0] == 1; a per-call
+            // ACM_REFERENCE_NEWTON sets NaN): rd and 1 / rd from rsq, sin / cos of rd w by sincos_0_2,
             // 1 / cos and 1 / |p| by rcp / rsq + Newton (~1-2 ulp each).  The
             // one decision, rd > sqrt(EPS) = 2^-26 (:320), is taken on r2
             // exactly: RN(sqrt(r2)) > 2^-26  <=>  r2 > 2^-52 (1 + 2^-52).

@@ -362,7 +362,12 @@ def leg_config4(ctx, n_total, reps):
     dev = torch.device("cuda", torch.cuda.current_device())
     L = _lib.load()
     sh = torch.cuda.current_stream().cuda_stream
-    pts = samples.synthetic_points_device(n, offset=lo)
+    # the global batch, then this rank's contiguous slice (the seeded
+    # generator's edge points depend on the batch size, so generating a
+    # shard on its own would not give the same points)
+    full = samples.synthetic_points_device(n_total)
+    pts = full[lo:hi].contiguous()
+    del full
     uv = torch.empty((max(n, 1), 2), dtype=torch.float64, device=dev)
     cams, outs = [], []
     for mid, name in LEG4_MODELS.items():

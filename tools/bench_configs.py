@@ -71,6 +71,32 @@ def config1():
           "valid": int((st == 0).sum()), "min_round_trip_dot": float(dots.min())})
 
 
+def lm_wall(src, xyz, uv, target, reps=5):
+    """The bounded LM alone (camera_converter.rs:381-420), from the linear
+    estimate: wall time of LevenbergMarquardt.optimize (every evaluation's
+    fused normal equations, the host solve and the host <-> device round
+    trip), the fastest of `reps` runs after one warm-up run."""
+    import torch
+    from apex_camera_models import conversion
+    from apex_camera_models.optimizer import CONVERTER_BOUNDS, LevenbergMarquardt
+    init = conversion._init_target(target, src)
+    init.linear_estimation(xyz, uv)
+    p0 = init.params()
+    best, res = float("inf"), None
+    for _ in range(reps + 1):
+        m = conversion._init_target(target, src)
+        m._set_params(list(p0))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = LevenbergMarquardt().optimize(m, xyz, uv, bounds=CONVERTER_BOUNDS[target])
+        best = min(best, time.perf_counter() - t0)
+    return {"what": f"bounded LM alone ({target}, from the linear estimate), wall",
+            "points": int(xyz.shape[0]), "lm_ms": round(best * 1e3, 3),
+            "iterations": res.iterations, "evaluations": res.evaluations,
+            "ms_per_evaluation": round(best * 1e3 / res.evaluations, 4),
+            "termination": res.termination}
+
+
 def config3(n_target):
     """DS residual+J and fused normal equations over ~10M KB-sampled
     correspondences, inside the bounded LM of camera_converter.rs:355-488."""
@@ -112,6 +138,7 @@ def config3(n_target):
     t0 = time.perf_counter()
     met = conversion.convert(src, "double_sphere", xyz, uv)
     t_conv = time.perf_counter() - t0
+    emit({"config": 3, **lm_wall(src, xyz, uv, "double_sphere")})
     emit({"config": 3, "what": "DS residual+J (2N x 6) kernel", "points": n,
           "ms": round(ms_rj, 4), "Mpoints_per_s": round(n / ms_rj / 1e3, 1),
           "GBps": round(153 * n / ms_rj / 1e6, 1)})
@@ -278,6 +305,7 @@ def config5(n_cells):
     t0 = time.perf_counter()
     met = conversion.convert(src, "double_sphere", xyz, uv)
     t_c = time.perf_counter() - t0
+    emit({"config": 5, **lm_wall(src, xyz, uv, "double_sphere", reps=2)})
     emit({"config": 5, "what": "KB->DS conversion (sample_points + linear_estimation + LM)",
           "requested": n_cells, "correspondences": n, "sample_points_s": round(t_s, 4),
           "convert_s": round(t_c, 4), "lm_iterations": met.lm_iterations,

@@ -151,8 +151,14 @@ def main():
     from apex_camera_models.camera import _stream_handle
     cells = 100_000_000
     cam = src.acm_camera()
-    su2 = torch.empty((cells, 2), dtype=torch.float64, device="cuda")
-    sx3 = torch.empty((cells, 3), dtype=torch.float64, device="cuda")
+    # outputs sized to the grid acm_sample_points actually uses (ncx * ncy
+    # may exceed the requested count; include/acm.h)
+    gx, gy = ctypes.c_uint32(), ctypes.c_uint32()
+    _lib.check(L.acm_sample_points_grid(cam.width, cam.height, cells, ctypes.byref(gx),
+                                        ctypes.byref(gy)))
+    cap = gx.value * gy.value
+    su2 = torch.empty((cap, 2), dtype=torch.float64, device="cuda")
+    sx3 = torch.empty((cap, 3), dtype=torch.float64, device="cuda")
     cnt = torch.zeros((2,), dtype=torch.int64, device="cuda")
     wsb = L.acm_sample_points_workspace_size(ctypes.byref(cam), cells)
     sws = torch.empty(((wsb + 7) // 8,), dtype=torch.float64, device="cuda")
