@@ -73,6 +73,7 @@ TUNE_NEWTON_FAST = 12  # removed in round 3: acm_set_tuning rejects it (use REFE
 TUNE_UNPROJECT_PPT = 13
 TUNE_SAMPLE_CERT = 14
 TUNE_SAMPLE_WRITE = 15
+TUNE_LM_DEVICE = 16  # r04: LM state machine on the device (k_lm_step)
 ERR_NOT_SUPPORTED = -6
 ERR_NUMERICAL = -7
 LM_TERMINATION = {0: "MaxIterations", 1: "CostTolerance", 2: "ParameterTolerance",
@@ -128,6 +129,7 @@ EXPORTED_SYMBOLS = (
     "acm_sample_points_range",
     "acm_sample_points_ex",
     "acm_sample_points_certificate",
+    "acm_sample_points_ray_fit",
     "acm_undistort_image",
     "acm_set_device",
     "acm_device_malloc",
@@ -211,6 +213,8 @@ def load():
     L.acm_sample_points_ex.restype = i
     L.acm_sample_points_certificate.argtypes = [cam_p, ctypes.POINTER(ctypes.c_double)]
     L.acm_sample_points_certificate.restype = i
+    L.acm_sample_points_ray_fit.argtypes = [cam_p, ctypes.POINTER(ctypes.c_double)]
+    L.acm_sample_points_ray_fit.restype = i
     L.acm_linear_system_columns.argtypes = [i]
     L.acm_linear_system_columns.restype = i
     L.acm_linear_system_qr_workspace_size.argtypes = [i, sz]

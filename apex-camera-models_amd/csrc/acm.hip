@@ -31,6 +31,7 @@
 
 #include "acm.h"
 #include "camera_models.hpp"
+#include "lm_core.hpp"
 
 namespace acm {
 
@@ -325,6 +326,12 @@ int lm_host_result() {
     const int v = g_lm_host_result.load(std::memory_order_relaxed);
     return v < 0 ? 2 : v;
 }
+// acm_lm_optimize without an all-reduce callback runs the LM state machine on
+// the device (k_lm_step behind each evaluation, r04): -1 = auto (= off until
+// measured faster), 0 = the host loop, 1 = on.  Bit-identical iterates
+// (lm_core.hpp).
+static std::atomic<int> g_lm_device{-1};
+int lm_device() { return g_lm_device.load(std::memory_order_relaxed) > 0; }
 // Outputs above this many bytes are stored non-temporally.  Measured at 10M
 // points (profiles/r01_diag_ntl.log): project without J (170 MB out) 0.056 ms
 // nt vs 0.072 plain; a consumer that re-reads a smaller output soon after
@@ -947,10 +954,21 @@ template <class TagT, int LAYOUT, int WAVES, int U, bool NTL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq(acm_camera cam, size_t n,
                                                       const double* __restrict__ pts,
                                                       const double* __restrict__ obs, int policy,
-                                                      double* __restrict__ parts) {
+                                                      double* __restrict__ parts,
+                                                      const double* __restrict__ dparams,
+                                                      const int* __restrict__ ddone) {
     using Acc = NeAccum<TagT>;
     constexpr int K = Acc::K;
-    const Cam<double> c = make_cam<double>(cam);
+    // the device-resident LM (r04): an evaluation queued after the run ended
+    // does nothing, and the parameters come from the previous k_lm_step (the
+    // projections read no host-derived constant of them; FOV's tan(w / 2)
+    // is one, so FOV keeps the host loop)
+    if (ddone && *ddone) return;
+    Cam<double> c = make_cam<double>(cam);
+    if (dparams) {
+#pragma unroll
+        for (int p = 0; p < Acc::P; ++p) c.p[p] = dparams[p];
+    }
     Acc sums;
     sums.init();
     const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
@@ -1132,6 +1150,36 @@ __global__ __launch_bounds__(kBlock) void k_ne_finish_cols(const double* __restr
 
 // The LM's host-polled path after k_ne_finish_cols: every result is out
 // (stream order), publish `seq` with a system-scope release.
+// One step of the device-resident LM (r04; lm_core.hpp): one thread takes
+// the evaluation k_ne_finish_cols just wrote (res), advances the state
+// machine to the next evaluation -- writing its parameters where the next
+// queued k_normal_eq reads them -- or ends the run (*ddone = 1), then
+// publishes the number of completed steps (and the end) in host-mapped
+// memory for the host's enqueue loop.  A step queued after the end returns
+// at once, so the host may run a few evaluations ahead.
+// The state is copied into registers (P is a template constant: every loop
+// of lm_core.hpp unrolls) and written back; the host reads only the two
+// flag words, so they need no release fence.
+template <int P>
+__global__ __launch_bounds__(64) void k_lm_step(lm::State* __restrict__ st, acm_lm_config cfg,
+                          const double* __restrict__ res, double* __restrict__ dparams,
+                          int* __restrict__ ddone, unsigned long long* __restrict__ hflag,
+                          unsigned long long seq) {
+    if (threadIdx.x != 0 || *ddone) return;
+    lm::State s = *st;
+    const int r = lm::consume(s, cfg, res, P);
+    *st = s;
+    if (r == lm::DONE) {
+        *ddone = 1;
+    } else {
+#pragma unroll
+        for (int p = 0; p < P; ++p) dparams[p] = s.xn[p];
+    }
+    __hip_atomic_store(hflag + 1, (unsigned long long)(r == lm::DONE), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(hflag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void k_ne_publish(unsigned long long* __restrict__ flag, unsigned long long seq) {
     __threadfence_system();
     __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1552,6 +1600,10 @@ struct SegCert {
     double all_lo, all_hi, none_lo, none_hi;
     double ig[9];  // KB: theta*(ru) ~= ru * sum ig[i] ru^(2i)
     double rp[2 * kRayPolyN];  // KB: cos theta*, sin theta* / ru ~= sum rp[i] r2^i, sum rp[N + i] r2^i
+    // KB: M = cmax / (2 dmin) of the Newton analysis, ef = the bound on
+    // |theta_ref - theta*| (the reference's final iterate vs the root, which
+    // the certified rays use), and the ray polynomials' sampled fit error
+    double M, ef, rp_err;
 };
 
 // Rigorous bounds of r2 = mx^2 + my^2 over the cells [c0, c1] (inclusive,
@@ -3281,6 +3333,8 @@ static SegCert kb_seg_cert_on(const double* p, double tmax) {
     const double m = ef + 1e-9;
     constexpr double kHpd = KannalaBrandt<double>::kHalfPiDown;
     s.on = 1;
+    s.M = M;
+    s.ef = ef;
     s.ig[0] = M;  // passed to kb_fit_initial_guess (overwritten by the fit)
     s.all_lo = 1e-6 * (1.0 + 1e-6);
     s.all_hi = R;
@@ -3305,7 +3359,11 @@ static SegCert kb_seg_cert_on(const double* p, double tmax) {
 // double).  Over 4001 points of the interval its error e0 decides
 // ray_certified's Newton steps: one when M e0^2 <= 1e-17 (M as in
 // kb_seg_cert_on), two when M^3 e0^4 <= 1e-13 and e0 <= 1e-5, else the fit
-// is not used (ig_ok = 0).
+// is not used (ig_ok = 0).  The error is SAMPLED (4001 points), not bounded.
+// Certified rays are the root's, the reference returns its last iterate:
+// they differ by up to ef = M (1.01e-6)^2 + 2 eta (kb_seg_cert_on), so the
+// rays are used only while ef <= 1e-11, a tenth of the 1e-10 bar (ADVICE
+// r03); otherwise every cell takes the reference-iterate path.
 static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
     s.ig_ok = 0;
     const long double k1 = p[4], k2 = p[5], k3 = p[6], k4 = p[7];
@@ -3355,6 +3413,7 @@ static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
         e0 = std::fmax(e0, std::fabs((double)((long double)ru * g - root(ru))));
     }
     s.ig_ok = M * e0 * e0 <= 1e-17 ? 1 : (e0 <= 1e-5 && M * M * M * e0 * e0 * e0 * e0 <= 1e-13 ? 2 : 0);
+    if (!(s.ef <= 1e-11)) s.ig_ok = 0;
 }
 
 // KB's certified-cell rays as polynomials in s = ru^2 on [0, all_hi^2]:
@@ -3363,9 +3422,13 @@ static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
 // function of ru), so degree 16 interpolants at Chebyshev nodes, solved in
 // long double (backward-stable elimination: the computed polynomials match
 // the node values to ~1e-18, and the Chebyshev nodes keep them as close in
-// between), reach rounding level; the error against long-double roots over
-// 4001 points of the interval must be <= 1e-13 (the rays are held to 1e-10)
-// or rp_ok stays 0 and ray_certified keeps its Newton form.
+// between), reach rounding level.  The fit is checked, not bounded: the
+// error against long-double roots on 16385 points of the interval (spacing
+// ~1.5e-4 of r2, against 16 node gaps) must be <= 1e-13, and with the
+// root-vs-reference distance ef, ef + error <= 1e-11 (the rays are held to
+// 1e-10), or rp_ok stays 0 and ray_certified keeps its Newton form (which the
+// ef gate of kb_fit_initial_guess covers in turn).  DESIGN.md §9 says
+// "sampled" for this check.
 static void kb_fit_ray(const double* p, SegCert& s) {
     s.rp_ok = 0;
     const long double k1 = p[4], k2 = p[5], k3 = p[6], k4 = p[7];
@@ -3416,8 +3479,9 @@ static void kb_fit_ray(const double* p, SegCert& s) {
         for (int i = 0; i < N; ++i) s.rp[which * N + i] = (double)(A[i][N] / A[i][i]);
     }
     double err = 0.0;
-    for (int i = 0; i <= 4000; ++i) {
-        const double sv = (double)Sm * i / 4000.0;
+    constexpr int kChecks = 16384;
+    for (int i = 0; i <= kChecks; ++i) {
+        const double sv = (double)Sm * i / kChecks;
         double C = s.rp[N - 1], S = s.rp[2 * N - 1];
         for (int k = N - 2; k >= 0; --k) {
             C = std::fma(C, sv, s.rp[k]);
@@ -3428,7 +3492,8 @@ static void kb_fit_ray(const double* p, SegCert& s) {
         err = std::fmax(err, std::fabs((double)(C - Ct)));
         err = std::fmax(err, std::fabs((double)(S - St)) * std::sqrt(sv));  // X = mx S, |m| = ru
     }
-    s.rp_ok = std::isfinite(err) && err <= 1e-13;
+    s.rp_err = err;
+    s.rp_ok = std::isfinite(err) && err <= 1e-13 && s.ef + err <= 1e-11;
 }
 
 static SegCert kb_seg_cert(const double* p) {
@@ -3793,10 +3858,13 @@ ACM_API size_t acm_normal_equations_workspace_size(int model, size_t n) {
 extern "C++" {
 namespace acm {
 // flag / seq: see k_ne_finish_cols / k_ne_publish (the LM's polled path in solver.hip)
+// dparams / ddone (the device-resident LM): parameters read by the kernel
+// from device memory, and the run's end flag (see k_normal_eq, k_lm_step).
 int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                           const double* points_2d_obs, int invalid_policy, double* result,
                           void* workspace, size_t workspace_bytes, void* stream,
-                          unsigned long long* flag, unsigned long long seq) {
+                          unsigned long long* flag, unsigned long long seq,
+                          const double* dparams, const int* ddone) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -3834,7 +3902,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
-                               points_2d_obs, invalid_policy, parts);
+                               points_2d_obs, invalid_policy, parts, dparams, ddone);
         };
         auto by_waves = [&](auto lay_c) {
             switch (wv) {
@@ -3856,6 +3924,24 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
         return check_launch("acm_normal_equations");
     });
 }
+
+int lm_step_launch(int P, lm::State* st, const acm_lm_config& cfg, const double* res,
+                   double* dparams, int* ddone, unsigned long long* hflag,
+                   unsigned long long seq, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, s, st, cfg, res, dparams, ddone, hflag, seq);
+    };
+    switch (P) {
+    case 4: go(k_lm_step<4>); break;
+    case 5: go(k_lm_step<5>); break;
+    case 6: go(k_lm_step<6>); break;
+    case 8: go(k_lm_step<8>); break;
+    case 9: go(k_lm_step<9>); break;
+    default: return fail(ACM_ERR_NOT_SUPPORTED, "LM step: unsupported parameter count");
+    }
+    return check_launch("acm_lm_optimize (k_lm_step)");
+}
 }  // namespace acm
 }  // extern "C++"
 
@@ -3864,7 +3950,8 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
                                  double* result, void* workspace, size_t workspace_bytes,
                                  void* stream) {
     return acm::normal_equations_impl(cam, n, points_3d, layout, points_2d_obs, invalid_policy,
-                                      result, workspace, workspace_bytes, stream, nullptr, 0);
+                                      result, workspace, workspace_bytes, stream, nullptr, 0,
+                                      nullptr, nullptr);
 }
 
 ACM_API size_t acm_reprojection_stats_workspace_size(size_t n) {
@@ -4156,6 +4243,23 @@ ACM_API int acm_sample_points_certificate(const acm_camera* cam, double* out) {
     out[2] = c.all_hi;
     out[3] = c.none_lo;
     out[4] = c.none_hi;
+    return ACM_SUCCESS;
+}
+
+ACM_API int acm_sample_points_ray_fit(const acm_camera* cam, double* out) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if (!out) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    for (int i = 0; i < 6; ++i) out[i] = 0.0;
+    if (cam->model != ACM_KANNALA_BRANDT) return ACM_SUCCESS;
+    const SegCert c = seg_cert(*cam);
+    const bool use = c.on && (c.ig_ok || c.rp_ok) && c.all_hi > c.all_lo;
+    out[0] = use ? (c.rp_ok ? 3 : c.ig_ok) : 0;
+    out[1] = c.on ? c.M : 0.0;
+    out[2] = c.on ? c.ef : 0.0;
+    out[3] = c.on ? c.rp_err : 0.0;
+    out[4] = c.all_lo;
+    out[5] = c.all_hi;
     return ACM_SUCCESS;
 }
 
@@ -4481,6 +4585,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_SAMPLE_CERT, &g_sample_cert, -1, 0, "value must be -1 (auto) or 0"},
         {ACM_TUNE_SAMPLE_WRITE, &g_sample_write, -1, 5, "value must be -1..5"},
         {ACM_TUNE_UNPROJECT_PPT, &g_unproject_ppt, -1, 3, "value must be -1..3"},
+        {ACM_TUNE_LM_DEVICE, &g_lm_device, -1, 1, "value must be -1..1"},
     };
     if (key == ACM_TUNE_NEWTON_FAST)  // removed (r03): numerics are chosen per call
         return fail(ACM_ERR_NOT_SUPPORTED,

@@ -13,12 +13,14 @@
 // reference's configuration; DESIGN.md documents the (unpinned) choice.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "acm.h"
+#include "lm_core.hpp"
 
 namespace acm {
 int set_error(int code, const std::string& msg);  // acm.hip (one last-error slot)
@@ -26,7 +28,12 @@ int lm_host_result();                              // acm.hip, ACM_TUNE_LM_HOST_
 int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                           const double* points_2d_obs, int invalid_policy, double* result,
                           void* workspace, size_t workspace_bytes, void* stream,
-                          unsigned long long* flag, unsigned long long seq);
+                          unsigned long long* flag, unsigned long long seq,
+                          const double* dparams, const int* ddone);
+int lm_device();                                   // acm.hip, ACM_TUNE_LM_DEVICE
+int lm_step_launch(int P, lm::State* st, const acm_lm_config& cfg, const double* res,
+                   double* dparams, int* ddone, unsigned long long* hflag,
+                   unsigned long long seq, void* stream);
 }
 
 namespace {
@@ -78,33 +85,6 @@ void svd_solve(int k, const double* A, const double* b, double eps, double* x) {
         const double coef = utb / (sj * sj);
         for (int i = 0; i < k; ++i) x[i] += V[i * k + j] * coef;
     }
-}
-
-bool cholesky_solve(int P, const double* A, const double* b, double* x) {
-    double L[81];
-    for (int i = 0; i < P; ++i)
-        for (int j = 0; j <= i; ++j) {
-            double s = A[i * P + j];
-            for (int q = 0; q < j; ++q) s -= L[i * P + q] * L[j * P + q];
-            if (i == j) {
-                if (!(s > 0.0)) return false;
-                L[i * P + i] = std::sqrt(s);
-            } else {
-                L[i * P + j] = s / L[j * P + j];
-            }
-        }
-    double y[9];
-    for (int i = 0; i < P; ++i) {
-        double s = b[i];
-        for (int q = 0; q < i; ++q) s -= L[i * P + q] * y[q];
-        y[i] = s / L[i * P + i];
-    }
-    for (int i = P - 1; i >= 0; --i) {
-        double s = y[i];
-        for (int q = i + 1; q < P; ++q) s -= L[q * P + i] * x[q];
-        x[i] = s / L[i * P + i];
-    }
-    return true;
 }
 
 int validate(const acm_camera* cam) {
@@ -311,10 +291,15 @@ ACM_API void acm_lm_default_config(acm_lm_config* cfg) {
     }
 }
 
+// LM workspace: the normal equations' partials | the results (R doubles + 8
+// spare) | the device-resident loop's state, parameters and end flag (r04).
+constexpr size_t kLmDevBytes = (sizeof(acm::lm::State) + 16 * sizeof(double) + 64 + 255) / 256 * 256;
+
 ACM_API size_t acm_lm_workspace_size(int model, size_t n) {
     const int P = acm_num_params(model);
     if (P < 0) return 0;
-    return acm_normal_equations_workspace_size(model, n) + (size_t)(P * P + P + 2 + 8) * 8;
+    return acm_normal_equations_workspace_size(model, n) + (size_t)(P * P + P + 2 + 8) * 8 +
+           kLmDevBytes;
 }
 
 ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, int layout,
@@ -332,7 +317,6 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
     double* d_res = (double*)((char*)workspace + ne_ws);
     const int R = P * P + P + 2;
     hipStream_t s = (hipStream_t)stream;
-    std::vector<double> h(R);
     // Without an all-reduce the epilogue kernel writes the R results straight
     // into pinned, device-mapped host memory: no device-to-host copy launch
     // per evaluation.  One buffer per host thread (calls on different threads
@@ -353,36 +337,29 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
     const int host_mode = allreduce ? 0 : acm::lm_host_result();
     double* res_out = d_res;
     unsigned long long* flag = nullptr;
-    if (host_mode) {
-        if (!pinned) {
-            void* p = nullptr;
-            if (hipHostMalloc(&p, 128 * sizeof(double),
-                              hipHostMallocMapped | hipHostMallocPortable |
-                                  hipHostMallocCoherent) == hipSuccess)
-                pinned = (double*)p;
-            else
-                (void)hipGetLastError();
-        }
-        if (pinned) {
-            res_out = pinned;
-            if (host_mode == 2) flag = reinterpret_cast<unsigned long long*>(pinned + 127);
-        }
+    // (the device-resident loop publishes its step count in words 120-121)
+    if (!allreduce && !pinned) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, 128 * sizeof(double),
+                          hipHostMallocMapped | hipHostMallocPortable |
+                              hipHostMallocCoherent) == hipSuccess)
+            pinned = (double*)p;
+        else
+            (void)hipGetLastError();
     }
-    acm_lm_summary sum;
-    std::memset(&sum, 0, sizeof(sum));
-
-    auto clamp = [&](double* x) {
-        if (!cfg->has_bounds) return;
-        for (int i = 0; i < P; ++i) x[i] = std::fmin(std::fmax(x[i], cfg->lower[i]), cfg->upper[i]);
-    };
-    // evaluate JtJ, Jtr, cost at parameter vector x
-    auto eval = [&](const double* x, double* A, double* g, double* F, double* nv) -> int {
+    if (host_mode && pinned) {
+        res_out = pinned;
+        if (host_mode == 2) flag = reinterpret_cast<unsigned long long*>(pinned + 127);
+    }
+    // evaluate [JtJ | Jtr | 0.5 r.r | n_valid] at parameter vector x (the
+    // host loop)
+    auto eval = [&](const double* x, double* out) -> int {
         acm_camera c = *cam;
         for (int i = 0; i < P; ++i) c.params[i] = x[i];
         const unsigned long long want = flag ? ++seq : 0;
         int rc = acm::normal_equations_impl(&c, n, points_3d, layout, points_2d,
                                             cfg->invalid_policy, res_out, workspace, ne_ws, stream,
-                                            flag, want);
+                                            flag, want, nullptr, nullptr);
         if (rc) return rc;
         if (allreduce) {
             rc = allreduce(allreduce_ctx, d_res, (size_t)R, stream);
@@ -403,109 +380,97 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
                 }
                 __builtin_ia32_pause();
             }
-            std::memcpy(h.data(), res_out, R * sizeof(double));
+            std::memcpy(out, res_out, R * sizeof(double));
         } else if (res_out != d_res) {
             if (hip_ok(hipStreamSynchronize(s))) return sfail(ACM_ERR_HIP, "LM: stream failed");
-            std::memcpy(h.data(), res_out, R * sizeof(double));
-        } else if (hip_ok(hipMemcpyAsync(h.data(), d_res, R * sizeof(double),
-                                         hipMemcpyDeviceToHost, s)) ||
+            std::memcpy(out, res_out, R * sizeof(double));
+        } else if (hip_ok(hipMemcpyAsync(out, d_res, R * sizeof(double), hipMemcpyDeviceToHost,
+                                         s)) ||
                    hip_ok(hipStreamSynchronize(s))) {
             return sfail(ACM_ERR_HIP, "LM: device copy failed");
         }
-        ++sum.evaluations;
-        std::memcpy(A, h.data(), P * P * sizeof(double));
-        for (int i = 0; i < P; ++i) g[i] = h[P * P + i];
-        *F = h[P * P + P];
-        *nv = h[P * P + P + 1];
         return ACM_SUCCESS;
     };
 
-    double x[9], A[81], g[9], F, nv;
-    for (int i = 0; i < P; ++i) x[i] = cam->params[i];
-    clamp(x);
-    int rc = eval(x, A, g, &F, &nv);
-    if (rc) return rc;
-    sum.initial_cost = F;
-    double dmax = 0.0;
-    for (int i = 0; i < P; ++i) dmax = std::fmax(dmax, A[i * P + i]);
-    double mu = cfg->initial_damping, nu = 2.0;
-    int term = ACM_LM_MAX_ITERATIONS;
-    auto ginf = [&](const double* gg) {
-        double m = 0.0;
-        for (int i = 0; i < P; ++i) m = std::fmax(m, std::fabs(gg[i]));
-        return m;
-    };
-    if (!std::isfinite(F)) term = ACM_LM_FAILED;
-    else if (ginf(g) <= cfg->gradient_tolerance) term = ACM_LM_GRADIENT;
-    int it = 0;
-    while (term == ACM_LM_MAX_ITERATIONS && it < cfg->max_iterations) {
-        ++it;
-        // (JtJ + mu * diag(JtJ)) h = -g   (Marquardt scaling, floored)
-        double Ad[81], mg[9], hstep[9];
-        for (int i = 0; i < P * P; ++i) Ad[i] = A[i];
-        for (int i = 0; i < P; ++i) {
-            Ad[i * P + i] += mu * std::fmax(A[i * P + i], 1e-12 * std::fmax(dmax, 1.0));
-            mg[i] = -g[i];
-        }
-        if (!cholesky_solve(P, Ad, mg, hstep)) {
-            mu *= nu;
-            nu *= 2.0;
-            continue;
-        }
-        double xn[9], xnorm = 0.0, hnorm = 0.0;
-        for (int i = 0; i < P; ++i) xn[i] = x[i] + hstep[i];
-        clamp(xn);
-        for (int i = 0; i < P; ++i) {
-            hstep[i] = xn[i] - x[i];
-            hnorm += hstep[i] * hstep[i];
-            xnorm += x[i] * x[i];
-        }
-        hnorm = std::sqrt(hnorm);
-        xnorm = std::sqrt(xnorm);
-        if (hnorm <= cfg->parameter_tolerance * (xnorm + cfg->parameter_tolerance)) {
-            term = ACM_LM_PARAMETER;
-            break;
-        }
-        double An[81], gn[9], Fn, nvn;
-        rc = eval(xn, An, gn, &Fn, &nvn);
-        if (rc) return rc;
-        // predicted reduction L(0) - L(h) = -(g.h + 0.5 h.A.h)
-        double gh = 0.0, hAh = 0.0;
-        for (int i = 0; i < P; ++i) {
-            gh += g[i] * hstep[i];
-            double t = 0.0;
-            for (int j = 0; j < P; ++j) t += A[i * P + j] * hstep[j];
-            hAh += hstep[i] * t;
-        }
-        const double pred = -(gh + 0.5 * hAh);
-        const double rho = (std::isfinite(Fn) && pred > 0.0) ? (F - Fn) / pred : -1.0;
-        if (rho > 0.0) {
-            const double dF = F - Fn;
-            const double Fold = F;
-            for (int i = 0; i < P; ++i) x[i] = xn[i];
-            std::memcpy(A, An, sizeof(double) * P * P);
-            std::memcpy(g, gn, sizeof(double) * P);
-            F = Fn;
-            nv = nvn;
-            const double t = 2.0 * rho - 1.0;
-            mu *= std::fmax(1.0 / 3.0, 1.0 - t * t * t);
-            nu = 2.0;
-            if (ginf(g) <= cfg->gradient_tolerance) term = ACM_LM_GRADIENT;
-            else if (dF <= cfg->cost_tolerance * Fold) term = ACM_LM_COST;
-        } else {
-            mu *= nu;
-            nu *= 2.0;
-            if (!std::isfinite(mu) || mu > 1e32) {
-                term = ACM_LM_FAILED;
-                break;
+    acm::lm::State st;
+    acm::lm::start(st, *cfg, P, cam->params);
+    // The device-resident loop (ACM_TUNE_LM_DEVICE, r04): each evaluation is
+    // k_normal_eq (parameters from device memory) -> k_ne_finish_cols ->
+    // k_lm_step, and the host keeps kAhead evaluations queued, watching the
+    // steps' count in host-mapped memory -- no host round trip between two
+    // evaluations.  Not with an all-reduce (the sums must pass through the
+    // host-side callback) nor for FOV (its projection reads tan(w / 2), a
+    // host-computed constant of the parameters).
+    const bool dev = acm::lm_device() && !allreduce && cam->model != ACM_FOV && pinned;
+    if (dev) {
+        char* base = (char*)workspace + need - kLmDevBytes;
+        acm::lm::State* d_st = reinterpret_cast<acm::lm::State*>(base);
+        double* d_par = reinterpret_cast<double*>(base + sizeof(acm::lm::State));
+        int* d_done = reinterpret_cast<int*>(d_par + 16);
+        unsigned long long* hflag = reinterpret_cast<unsigned long long*>(pinned + 120);
+        __atomic_store_n(hflag, 0ull, __ATOMIC_RELEASE);
+        __atomic_store_n(hflag + 1, 0ull, __ATOMIC_RELEASE);
+        const int zero = 0;
+        if (hip_ok(hipMemcpyAsync(d_st, &st, sizeof(st), hipMemcpyHostToDevice, s)) ||
+            hip_ok(hipMemcpyAsync(d_par, st.xn, 9 * sizeof(double), hipMemcpyHostToDevice, s)) ||
+            hip_ok(hipMemcpyAsync(d_done, &zero, sizeof(int), hipMemcpyHostToDevice, s)) ||
+            hip_ok(hipStreamSynchronize(s)))
+            return sfail(ACM_ERR_HIP, "LM: device state upload failed");
+        constexpr unsigned long long kAhead = 2;
+        const unsigned long long max_evals = (unsigned long long)std::max(cfg->max_iterations, 0) + 1;
+        unsigned long long queued = 0;
+        auto enqueue = [&]() -> int {
+            int rc = acm::normal_equations_impl(cam, n, points_3d, layout, points_2d,
+                                                cfg->invalid_policy, d_res, workspace, ne_ws,
+                                                stream, nullptr, 0, d_par, d_done);
+            if (rc) return rc;
+            return acm::lm_step_launch(P, d_st, *cfg, d_res, d_par, d_done, hflag, ++queued,
+                                       stream);
+        };
+        int rc = ACM_SUCCESS;
+        while (queued < max_evals) {
+            // keep at most kAhead evaluations in flight; stop at the end
+            bool done = false;
+            for (unsigned spin = 1;; ++spin) {
+                const unsigned long long got = __atomic_load_n(hflag, __ATOMIC_ACQUIRE);
+                done = __atomic_load_n(hflag + 1, __ATOMIC_ACQUIRE) != 0;
+                if (done || got + kAhead > queued) break;
+                if ((spin & 255) == 0) {
+                    const hipError_t q = hipStreamQuery(s);
+                    if (q == hipSuccess) {
+                        if (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) + kAhead > queued ||
+                            __atomic_load_n(hflag + 1, __ATOMIC_ACQUIRE))
+                            continue;
+                        return sfail(ACM_ERR_HIP, "LM: step count not published");
+                    }
+                    if (q != hipErrorNotReady) return sfail(ACM_ERR_HIP, "LM: stream failed");
+                }
+                __builtin_ia32_pause();
             }
+            if (done) break;
+            if ((rc = enqueue())) return rc;
+        }
+        if (hip_ok(hipMemcpyAsync(&st, d_st, sizeof(st), hipMemcpyDeviceToHost, s)) ||
+            hip_ok(hipStreamSynchronize(s)))
+            return sfail(ACM_ERR_HIP, "LM: device state download failed");
+    } else {
+        std::vector<double> res(R);
+        int r = acm::lm::NEED_EVAL;
+        while (r == acm::lm::NEED_EVAL) {
+            int rc = eval(st.xn, res.data());
+            if (rc) return rc;
+            r = acm::lm::consume(st, *cfg, res.data(), P);
         }
     }
-    for (int i = 0; i < P; ++i) cam->params[i] = x[i];
-    sum.iterations = it;
-    sum.termination = term;
-    sum.final_cost = F;
-    sum.n_valid = nv;
+    for (int i = 0; i < P; ++i) cam->params[i] = st.x[i];
+    acm_lm_summary sum;
+    std::memset(&sum, 0, sizeof(sum));
+    sum.iterations = st.it;
+    sum.termination = st.term;
+    sum.evaluations = st.evals;
+    sum.initial_cost = st.initial_cost;
+    sum.final_cost = st.F;
+    sum.n_valid = st.nv;
     if (summary) *summary = sum;
     return ACM_SUCCESS;
 }

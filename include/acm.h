@@ -385,6 +385,16 @@ ACM_API int acm_sample_points_range(const acm_camera *cam, size_t n_requested,
  * [none_lo, none_hi]; on = 0: no certificate (every segment is counted cell
  * by cell).  Host only. */
 ACM_API int acm_sample_points_certificate(const acm_camera *cam, double *out);
+/* (r04) KB only: how acm_sample_points forms the rays of cells inside the
+ * certified kept interval.  out = [mode, M, ef, fit_err, all_lo, all_hi]:
+ * mode 0 = the reference-iterate path for every cell, 1 / 2 = the root by
+ * the fitted initial guess + 1 / 2 Newton steps, 3 = the ray polynomials;
+ * M = the Newton error constant, ef = the bound on the distance between the
+ * reference's final iterate and the root the certified rays use (modes 1-3
+ * require ef <= 1e-11), fit_err = the ray polynomials' error, sampled on
+ * 16385 points (mode 3 requires <= 1e-13).  Zeros for other models.  Host
+ * only. */
+ACM_API int acm_sample_points_ray_fit(const acm_camera *cam, double *out);
 
 /* acm_sample_points_range with per-call options: flags = 0 or
  * ACM_REFERENCE_NEWTON.  (acm_sample_points / _range = flags 0.) */
@@ -482,6 +492,12 @@ ACM_API int acm_stream_synchronize(void *stream);
  * 16-B aligned; 1 / 2 = pixels per lane with three 8-B stores per ray; 3 =
  * 1 pixel per lane, staged when rays is 16-B aligned).
  * Outputs are identical for every value.
+ * ACM_TUNE_LM_DEVICE (r04): acm_lm_optimize without an all-reduce callback
+ * keeps the LM's state on the device -- a one-thread step kernel behind each
+ * evaluation's normal equations computes the next trial point, and the host
+ * only keeps two evaluations queued ahead -- instead of a host round trip
+ * per evaluation: -1 = auto = on, 0 = the host loop, 1 = on.  The same
+ * state machine (lm_core.hpp) either way: bit-identical iterates.
  * Every knob is an atomic: acm_set_tuning may race with any other call.
  * Returns the previous value or an error. */
 enum {
@@ -500,7 +516,8 @@ enum {
     ACM_TUNE_NEWTON_FAST = 12,
     ACM_TUNE_UNPROJECT_PPT = 13,
     ACM_TUNE_SAMPLE_CERT = 14,
-    ACM_TUNE_SAMPLE_WRITE = 15
+    ACM_TUNE_SAMPLE_WRITE = 15,
+    ACM_TUNE_LM_DEVICE = 16
 };
 ACM_API int acm_set_tuning(int key, int value);
 

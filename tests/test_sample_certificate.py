@@ -88,3 +88,41 @@ def test_strong_distortion_partial_certificate():
     on, alo, ahi, nlo, nhi = cert(params)
     assert on == 1 and max(ahi, nhi) < math.pi / 2
     assert _check(params)
+
+
+def ray_fit(params, w=512, h=512):
+    L = _lib.load()
+    cam = _lib.AcmCamera()
+    _lib.check(L.acm_camera_init(ctypes.byref(cam), 2, (ctypes.c_double * 8)(*params), 8, w, h))
+    out = (ctypes.c_double * 6)()
+    _lib.check(L.acm_sample_points_ray_fit(ctypes.byref(cam), out))
+    return list(out)
+
+
+def test_ray_fit_gates():
+    """acm_sample_points_ray_fit (r04): the certified rays (the
+    root theta*, not the reference's last iterate) are used only while the
+    root-vs-iterate bound ef <= 1e-11, and the ray polynomials only while
+    their sampled error <= 1e-13; on the sample camera both hold."""
+    mode, M, ef, err, lo, hi = ray_fit(KB_SAMPLE)
+    assert mode == 3 and ef <= 1e-11 and 0 < err <= 1e-13 and lo < hi
+    rng = np.random.default_rng(11)
+    modes = []
+    for _ in range(60):
+        dist = list(rng.normal(0, [0.2, 0.1, 0.05, 0.02]))
+        mode, M, ef, err, lo, hi = ray_fit([200.0, 200.0, 256.0, 256.0] + dist)
+        modes.append(mode)
+        if mode:
+            assert ef <= 1e-11, (dist, ef)
+            assert abs(M * 1.01e-6 ** 2 - ef) <= ef  # ef = M (1.01e-6)^2 + 2 eta
+        if mode == 3:
+            assert err <= 1e-13 and ef + err <= 1e-11
+    assert 0 in modes or min(modes) >= 1  # both outcomes are legal; the gates held
+    # non-KB models report zeros
+    L = _lib.load()
+    cam = _lib.AcmCamera()
+    _lib.check(L.acm_camera_init(ctypes.byref(cam), 0, (ctypes.c_double * 4)(
+        500.0, 500.0, 320.0, 240.0), 4, 640, 480))
+    out = (ctypes.c_double * 6)()
+    _lib.check(L.acm_sample_points_ray_fit(ctypes.byref(cam), out))
+    assert list(out) == [0.0] * 6

@@ -1,8 +1,9 @@
 """LM loop overhead on config-3 data (KB-sampled correspondences, DS target):
 wall time of acm_lm_optimize vs evaluations x the normal-equation kernel
-time, i.e. the host / launch / copy cost per evaluation, for each
-ACM_TUNE_LM_HOST_RESULT mode (0 copy + sync, 1 pinned + sync, 2 pinned +
-spin on the completion word; the reported wall is mode 2, the default).
+time, i.e. the host / launch / copy cost per evaluation, for the
+device-resident loop (ACM_TUNE_LM_DEVICE, r04: "dev") and the host loop with
+each ACM_TUNE_LM_HOST_RESULT mode (0 copy + sync, 1 pinned + sync, 2 pinned
++ spin on the completion word); the reported wall is the default.
 
   python tools/diag_lm.py [--points N]
 """
@@ -49,9 +50,11 @@ def main():
     L = _lib.load()
     by_mode = {}
     res = None
+    modes = {"dev": (1, -1), "host0": (0, 0), "host1": (0, 1), "host2": (0, 2)}
     for _ in range(3):
-        for mode in (0, 1, 2):  # ACM_TUNE_LM_HOST_RESULT: copy / pinned + sync / pinned + spin
-            L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, mode)
+        for mode, (dev, host) in modes.items():
+            L.acm_set_tuning(_lib.TUNE_LM_DEVICE, dev)
+            L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, host)
             m = conversion._init_target("double_sphere", src)
             m._set_params(list(p0))
             torch.cuda.synchronize()
@@ -62,9 +65,10 @@ def main():
             ms = (time.perf_counter() - t0) * 1e3
             by_mode[mode] = min(by_mode.get(mode, 1e9), ms)
     L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, -1)
-    wall = by_mode[2]
+    L.acm_set_tuning(_lib.TUNE_LM_DEVICE, -1)
+    wall = by_mode["dev"]
     print(json.dumps({"what": "LM loop overhead", "points": n, "lm_wall_ms": round(wall, 3),
-                      "lm_wall_ms_by_host_result_mode": {k: round(v, 3) for k, v in by_mode.items()},
+                      "lm_wall_ms_by_mode": {k: round(v, 3) for k, v in by_mode.items()},
                       "evaluations": res.evaluations, "iterations": res.iterations,
                       "ne_ms": round(ne_ms, 4),
                       "overhead_per_eval_ms": round((wall - res.evaluations * ne_ms)

@@ -48,7 +48,8 @@ for step in "$@"; do
   [[ "$step" == *=* ]] && arg=${step#*=}
   case "$name" in
   tests)
-    timeout -k 10 900 python -u -m pytest ${arg:-tests} -m gpu -q --timeout 300 \
+    targs=${arg//+/ }
+    timeout -k 10 900 python -u -m pytest ${targs:-tests} -m gpu -q --timeout 300 \
       --timeout-method thread -rf > $O/${TAG}_pytest_gpu.log 2>&1
     check $? tests; tail -n 2 $O/${TAG}_pytest_gpu.log ;;
   smoke)
