@@ -1166,9 +1166,30 @@ __global__ __launch_bounds__(64) void k_lm_step(lm::State* __restrict__ st, acm_
                           int* __restrict__ ddone, unsigned long long* __restrict__ hflag,
                           unsigned long long seq) {
     if (threadIdx.x != 0 || *ddone) return;
-    lm::State s = *st;
+    // The one working lane reads the state and the results through an
+    // opaque (divergent) lane offset, 0 here: uniform loads would put the
+    // ~140 doubles in SGPRs, where FP64 cannot be computed on, and spill
+    // (hundreds of SGPR spills to scratch).  Element-wise copies with
+    // constant indices then split the state into VGPRs.
+    unsigned off = threadIdx.x;
+    asm volatile("" : "+v"(off));
+    st += off;
+    res += off;
+    lm::State s;
+    auto io = [&](lm::State& d, const lm::State& a) {
+        d.P = a.P; d.it = a.it; d.evals = a.evals; d.term = a.term; d.phase = a.phase;
+        d.F = a.F; d.nv = a.nv; d.mu = a.mu; d.nu = a.nu; d.dmax = a.dmax;
+        d.initial_cost = a.initial_cost;
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            d.x[i] = a.x[i]; d.xn[i] = a.xn[i]; d.h[i] = a.h[i]; d.g[i] = a.g[i];
+        }
+#pragma unroll
+        for (int i = 0; i < P * P; ++i) d.A[i] = a.A[i];
+    };
+    io(s, *st);
     const int r = lm::consume(s, cfg, res, P);
-    *st = s;
+    io(*st, s);
     if (r == lm::DONE) {
         *ddone = 1;
     } else {
