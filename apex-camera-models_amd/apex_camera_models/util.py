@@ -81,16 +81,28 @@ def reprojection_stats(camera_model: CameraModel, points3d, points2d, errors=Non
 
 
 def compute_reprojection_error(camera_model: CameraModel, points3d, points2d) -> ProjectionError:
-    """error_metrics.rs:62-121 (median: see reprojection_median)."""
+    """error_metrics.rs:62-121: one acm_reprojection_error call (the
+    statistics and the median, whose first radix histogram the statistics
+    pass counts) and one device -> host read of its 9 doubles."""
+    L = _lib.load()
     p3 = _as_device_f64(points3d, 3)
-    errors = torch.empty((p3.shape[0],), dtype=torch.float64, device=p3.device)
-    out = reprojection_stats(camera_model, p3, points2d, errors).cpu().tolist()
+    p2 = _as_device_f64(points2d, 2)
+    n = p3.shape[0]
+    if p2.shape[0] != n:
+        raise ValueError("points3d and points2d must have the same number of columns")
+    ws_bytes = L.acm_reprojection_error_workspace_size(n)
+    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=p3.device)
+    res = torch.empty((9,), dtype=torch.float64, device=p3.device)
+    cam = camera_model.acm_camera()
+    _lib.check(L.acm_reprojection_error(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
+                                        p2.data_ptr(), res.data_ptr(), None, ws.data_ptr(),
+                                        ws_bytes, _stream_handle()))
+    out = res.cpu().tolist()
     n_valid = int(out[5])
     if n_valid == 0:
         raise ZeroProjectionPoints()
-    median = reprojection_median(errors, n_valid)
     return ProjectionError(rmse=out[0], min=out[1], max=out[2], mean=out[3], stddev=out[4],
-                           median=median, n_valid=n_valid)
+                           median=out[8], n_valid=n_valid)
 
 
 def reprojection_median(errors: torch.Tensor, n_valid: int) -> float:
@@ -170,9 +182,14 @@ def validate_conversion_accuracy(output_model: CameraModel,
     rays, st_u = input_model.unproject_batch(pix)
     uv_in, st_in, _ = input_model.project_batch(rays)
     uv_out, st_out, _ = output_model.project_batch(rays)
-    rays_ok = st_u.cpu().tolist()
-    ok_in, ok_out = st_in.cpu().tolist(), st_out.cpu().tolist()
-    a, b = uv_in.cpu().tolist(), uv_out.cpu().tolist()
+    # one device -> host read for all five outputs (each .cpu() is a sync)
+    k = len(_REGIONS)
+    flat = torch.cat([st_u.reshape(-1).to(torch.float64), st_in.reshape(-1).to(torch.float64),
+                      st_out.reshape(-1).to(torch.float64), uv_in.reshape(-1),
+                      uv_out.reshape(-1)]).cpu().tolist()
+    rays_ok, ok_in, ok_out = flat[:k], flat[k:2 * k], flat[2 * k:3 * k]
+    a = [flat[3 * k + 2 * j: 3 * k + 2 * j + 2] for j in range(k)]
+    b = [flat[5 * k + 2 * j: 5 * k + 2 * j + 2] for j in range(k)]
     total, max_error, valid = 0.0, 0.0, 0
     errs, data = [], []
     for i, (name, _) in enumerate(_REGIONS):

@@ -1272,70 +1272,119 @@ __device__ __forceinline__ void reproj_block_store(double s, double ss, double m
     }
 }
 
+// The median's radix digits (see "median" below): 11 bits, 2048 bins.
+constexpr int kSelBits = 11, kSelBins = 1 << kSelBits;
+
+// One LDS histogram increment per lane with pred, aggregated across the wave
+// when AGG: lanes holding the same digit add their count with one atomic
+// (pass 0's digits are the exponent: a wave's 64 values share a handful of
+// them, and 64 same-address LDS atomics would serialise).
+template <bool AGG>
+__device__ __forceinline__ void sel_count(unsigned int* h, bool pred, unsigned d) {
+    if (!AGG) {
+        if (pred) atomicAdd(&h[d], 1u);
+        return;
+    }
+    unsigned long long act = __ballot(pred);
+    const int lane = threadIdx.x & 63;
+    while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const unsigned dl = (unsigned)__shfl((int)d, leader, 64);
+        const unsigned long long same = __ballot(pred && d == dl) & act;
+        if (lane == leader) atomicAdd(&h[dl], (unsigned)__popcll(same));
+        act &= ~same;
+    }
+}
+
 // e_i = ||proj(p_i) - uv_i|| (NaN if the projection fails); per-workgroup
-// partials (kReprojW doubles).  NTS: non-temporal error stores.
-template <class TagT, int LAYOUT, bool NTL, bool NTS>
+// partials (kReprojW doubles).  NTS: non-temporal error stores.  Software
+// pipelined like k_normal_eq (r04): one point per lane step, the loads of the
+// next kReprojA steps in flight in static slots, branch-free (past the end:
+// point n - 1 again, never used) -- 2 points per lane per chunk without
+// prefetch ran 4.96 TB/s at 92.9M (profiles/r04j_convert_kernel_stats.csv).
+// HIST (acm_reprojection_error): the median's first radix-select histogram
+// (the 11-bit digit of bits 53..63 of every error, NaN included, exactly
+// k_sel_hist's pass 0) is counted here in LDS and written per workgroup to
+// hparts (2048 u32), which saves the median one full read of the errors.
+constexpr int kReprojA = 2;
+
+template <class TagT, int LAYOUT, bool NTL, bool NTS, bool HIST>
 __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t n,
                                                          const double* __restrict__ pts,
                                                          const double* __restrict__ obs,
                                                          double* __restrict__ errs,
-                                                         double* __restrict__ parts) {
+                                                         double* __restrict__ parts,
+                                                         unsigned int* __restrict__ hparts) {
     using M = typename TagT::template type<double>;
+    constexpr int HB = kSelBins;
+    __shared__ unsigned int h[HIST ? HB : 1];
+    if constexpr (HIST) {
+        for (int j = threadIdx.x; j < HB; j += kBlock) h[j] = 0;
+        __syncthreads();
+    }
     const Cam<double> c = make_cam<double>(cam);
     double s = 0.0, ss = 0.0, mn = INFINITY, mx = -INFINITY, cnt = 0.0;
     double K = 0.0, S = 0.0, Q = 0.0;  // shifted sums about this lane's first valid error
-    // each wave streams contiguous chunks of kReprojU x 64 points
-    const size_t nw = (size_t)gridDim.x * (kBlock / 64);
-    constexpr size_t C = (size_t)kReprojU * 64;
-    for (size_t b0 = ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * C; b0 < n;
-         b0 += nw * C) {
-        double x[kReprojU], y[kReprojU], z[kReprojU];
-        double2 o[kReprojU];
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    constexpr int A = kReprojA;
+    double xs[A], ys[A], zs[A];
+    double2 os[A];
+    auto load_slot = [&](int q, size_t iq) {
+        const size_t ic = iq < n ? iq : n - 1;
+        load_point<LAYOUT, NTL>(pts, n, ic, xs[q], ys[q], zs[q]);
+        os[q] = ld2<NTL>(obs + 2 * ic);
+    };
+    if (n) {
 #pragma unroll
-        for (int k = 0; k < kReprojU; ++k) {
-            const size_t i = b0 + k * 64 + (threadIdx.x & 63);
-            x[k] = 0.0; y[k] = 0.0; z[k] = 1.0;
-            o[k] = make_double2(0.0, 0.0);
-            if (i < n) {
-                load_point<LAYOUT, NTL>(pts, n, i, x[k], y[k], z[k]);
-                o[k] = ld2<NTL>(obs + 2 * i);
-            }
-        }
+        for (int q = 0; q < A; ++q) load_slot(q, i + (size_t)q * stride);
+    }
+    for (; i < n; i += (size_t)A * stride) {
 #pragma unroll
-        for (int k = 0; k < kReprojU; ++k) {
-            const size_t i = b0 + k * 64 + (threadIdx.x & 63);
-            if (i >= n) break;
-            double u, v;
-            const uint8_t st = M::template project<false>(c, x[k], y[k], z[k], u, v, nullptr,
-                                                          nullptr);
+        for (int q = 0; q < A; ++q) {
+            const size_t iq = i + (size_t)q * stride;
+            const bool in = iq < n;
             double e = __builtin_nan("");
-            if (st == ST_OK) {
-                const double du = u - o[k].x, dv = v - o[k].y;
-                e = sqrt(du * du + dv * dv);
+            if (in) {
+                double u, v;
+                const uint8_t st = M::template project<false>(c, xs[q], ys[q], zs[q], u, v,
+                                                              nullptr, nullptr);
+                if (st == ST_OK) {
+                    const double du = u - os[q].x, dv = v - os[q].y;
+                    e = sqrt(du * du + dv * dv);
+                }
+                // One validity rule for the statistics and the median: an Ok
+                // projection whose error is NaN (a NaN observation) is not a
+                // valid error -- acm_median_valid skips NaN too.  (The
+                // reference would sum the NaN and then panic in its median
+                // sort, error_metrics.rs:104-108 partial_cmp().unwrap().)
+                if (e == e) {
+                    s += e;
+                    ss += e * e;
+                    mn = fmin(mn, e);
+                    mx = fmax(mx, e);
+                    K = cnt == 0.0 ? e : K;
+                    const double d = e - K;
+                    S += d;
+                    Q += d * d;
+                    cnt += 1.0;
+                }
+                if (NTS) __builtin_nontemporal_store(e, errs + iq);
+                else errs[iq] = e;
             }
-            // One validity rule for the statistics and the median: an Ok
-            // projection whose error is NaN (a NaN observation) is not a
-            // valid error -- acm_median_valid skips NaN too.  (The reference
-            // would sum the NaN and then panic in its median sort,
-            // error_metrics.rs:104-108 partial_cmp().unwrap().)
-            if (e == e) {
-                s += e;
-                ss += e * e;
-                mn = fmin(mn, e);
-                mx = fmax(mx, e);
-                K = cnt == 0.0 ? e : K;
-                const double d = e - K;
-                S += d;
-                Q += d * d;
-                cnt += 1.0;
-            }
-            if (NTS) __builtin_nontemporal_store(e, errs + i);
-            else errs[i] = e;
+            if constexpr (HIST)
+                sel_count<true>(h, in, (unsigned)(((unsigned long long)__double_as_longlong(e) >> 53) & (HB - 1)));
+            load_slot(q, iq + (size_t)A * stride);
         }
     }
     const double mloc = cnt > 0.0 ? S / cnt : 0.0;
     const Mv v{cnt, K + mloc, cnt > 0.0 ? Q - S * mloc : 0.0};
     reproj_block_store(s, ss, mn, mx, v, parts + (size_t)blockIdx.x * kReprojW);
+    if constexpr (HIST) {
+        __syncthreads();
+        unsigned int* hp = hparts + (size_t)blockIdx.x * HB;
+        for (int j = threadIdx.x; j < HB; j += kBlock) hp[j] = h[j];
+    }
 }
 
 // The same per-workgroup partials from a given error vector (NaN = invalid):
@@ -2286,33 +2335,11 @@ struct SelState {
 // 2 x 8 with 8-bit digits).  Histogram counts are kept as f64 (exact below
 // 2^53, and integer sums are order-independent) so a multi-GPU caller can
 // all-reduce them in place with the same f64 callback the LM uses.
-constexpr int kSelBits = 11, kSelBins = 1 << kSelBits;
 // digit p covers bits [shift, shift + width): 53..63, 42..52, 31..41, 20..30, 9..19, 0..8
 __host__ __device__ constexpr int sel_shift(int pass) { return pass < 5 ? 53 - 11 * pass : 0; }
 __host__ __device__ constexpr int sel_width(int pass) { return pass < 5 ? 11 : 9; }
 constexpr int kSelPasses = 6;
 constexpr int kSelU = 8;  // values in flight per lane in the streaming passes
-
-// One LDS histogram increment per lane with pred, aggregated across the wave
-// when AGG: lanes holding the same digit add their count with one atomic
-// (pass 0's digits are the exponent: a wave's 64 values share a handful of
-// them, and 64 same-address LDS atomics would serialise).
-template <bool AGG>
-__device__ __forceinline__ void sel_count(unsigned int* h, bool pred, unsigned d) {
-    if (!AGG) {
-        if (pred) atomicAdd(&h[d], 1u);
-        return;
-    }
-    unsigned long long act = __ballot(pred);
-    const int lane = threadIdx.x & 63;
-    while (act) {
-        const int leader = __ffsll((long long)act) - 1;
-        const unsigned dl = (unsigned)__shfl((int)d, leader, 64);
-        const unsigned long long same = __ballot(pred && d == dl) & act;
-        if (lane == leader) atomicAdd(&h[dl], (unsigned)__popcll(same));
-        act &= ~same;
-    }
-}
 
 // The streaming selection kernels run one 1024-lane workgroup per CU: 16
 // waves x kSelU loads in flight per CU, and only #CU workgroups flushing
@@ -2367,6 +2394,23 @@ __global__ __launch_bounds__(kSelBlock) void k_sel_hist(size_t n, const unsigned
         const unsigned c1 = same ? c0 : h[1][j];
         if (c0) atomicAdd(&hist[j], (double)c0);
         if (c1) atomicAdd(&hist[kSelBins + j], (double)c1);
+    }
+}
+
+// Pass 0's histogram from the per-workgroup counts of k_reproj_pass1<HIST>
+// (nb x 2048 u32): grid (kSelBins / kBlock, kSelMergeG); each lane sums one
+// bin over every kSelMergeG-th workgroup, then one f64 atomic per non-zero
+// bin and group into both states' halves (k_sel_init zeroed them; integer
+// sums, so the order of the atomics does not matter).
+constexpr int kSelMergeG = 64;
+__global__ __launch_bounds__(kBlock) void k_sel_hist_merge(const unsigned int* __restrict__ hparts,
+                                                           int nb, double* __restrict__ hist) {
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    unsigned long long c = 0;
+    for (int b = blockIdx.y; b < nb; b += kSelMergeG) c += hparts[(size_t)b * kSelBins + j];
+    if (c) {
+        atomicAdd(&hist[j], (double)c);
+        atomicAdd(&hist[kSelBins + j], (double)c);
     }
 }
 
@@ -3981,18 +4025,15 @@ ACM_API size_t acm_reprojection_stats_workspace_size(size_t n) {
     return (n + nb * kReprojW + kReprojW) * sizeof(double);
 }
 
-ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double* points_3d,
+// hparts != nullptr: also the median's first histogram per workgroup
+// (k_reproj_pass1<HIST>); *nb_out = the workgroups launched
+static int reprojection_stats_impl(const acm_camera* cam, size_t n, const double* points_3d,
                                    int layout, const double* points_2d, double* result,
-                                   double* errors, void* workspace, size_t workspace_bytes,
-                                   void* stream) {
+                                   double* errors, void* workspace, hipStream_t s,
+                                   unsigned int* hparts, int* nb_out) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
-    if (!result || !workspace || (n && (!points_3d || !points_2d)))
-        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
-    if (workspace_bytes < acm_reprojection_stats_workspace_size(n))
-        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "reprojection-stats workspace too small");
-    hipStream_t s = (hipStream_t)stream;
     const int nb_max = ne_blocks(n);
     double* ws = (double*)workspace;
     double* errs = errors ? errors : ws;
@@ -4005,20 +4046,39 @@ ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double
         const bool nts = n * sizeof(double) > kNtThresholdBytes;
         auto go = [&](auto lay_c) {
             constexpr int LAY = decltype(lay_c)::value;
-            auto kern = ntl ? k_reproj_pass1<TagT, LAY, true, false>
-                            : k_reproj_pass1<TagT, LAY, false, false>;
-            if (nts) kern = ntl ? k_reproj_pass1<TagT, LAY, true, true>
-                                : k_reproj_pass1<TagT, LAY, false, true>;
+            auto kern = ntl ? k_reproj_pass1<TagT, LAY, true, false, false>
+                            : k_reproj_pass1<TagT, LAY, false, false, false>;
+            if (nts) kern = ntl ? k_reproj_pass1<TagT, LAY, true, true, false>
+                                : k_reproj_pass1<TagT, LAY, false, true, false>;
+            if (hparts) {
+                kern = ntl ? k_reproj_pass1<TagT, LAY, true, false, true>
+                           : k_reproj_pass1<TagT, LAY, false, false, true>;
+                if (nts) kern = ntl ? k_reproj_pass1<TagT, LAY, true, true, true>
+                                    : k_reproj_pass1<TagT, LAY, false, true, true>;
+            }
             nb1 = std::min(nb1, resident_blocks(reinterpret_cast<const void*>(kern)));
             hipLaunchKernelGGL(kern, dim3(nb1), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
-                               points_2d, errs, p1);
+                               points_2d, errs, p1, hparts);
         };
         if (layout == ACM_LAYOUT_AOS) go(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else go(std::integral_constant<int, ACM_LAYOUT_SOA>{});
         hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb1, tot);
         hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, result);
+        if (nb_out) *nb_out = nb1;
         return check_launch("acm_reprojection_stats");
     });
+}
+
+ACM_API int acm_reprojection_stats(const acm_camera* cam, size_t n, const double* points_3d,
+                                   int layout, const double* points_2d, double* result,
+                                   double* errors, void* workspace, size_t workspace_bytes,
+                                   void* stream) {
+    if (!result || !workspace || (n && (!points_3d || !points_2d)))
+        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_reprojection_stats_workspace_size(n))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "reprojection-stats workspace too small");
+    return reprojection_stats_impl(cam, n, points_3d, layout, points_2d, result, errors,
+                                   workspace, (hipStream_t)stream, nullptr, nullptr);
 }
 
 ACM_API size_t acm_error_stats_workspace_size(size_t n) {
@@ -4192,11 +4252,13 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
             // interleaved, 3 = 4 interleaved, 4 = 16 contiguous, 5 = 16
             // interleaved with non-temporal stores)
             // auto: 4 segments per wave for the cheapest unprojections (UCM,
-            // EUCM, FOV: 0.71 vs 0.84 ms at 1e8 cells), 16 for the rest (KB
-            // 0.82 vs 0.95, DS 0.81 vs 0.86; profiles/r03f_diag_sample.log)
+            // EUCM, FOV: 0.71 vs 0.84 ms at 1e8 cells) and, since its rays
+            // come from the LDS-staged polynomials (r04), for KB (0.745 vs
+            // 0.847 ms, profiles/r04j_sample_write_layout.log); 16 for DS
+            // (0.787 vs 0.827) and Pinhole (0.763 vs 0.752, even)
             const int wv0 = g_sample_write.load(std::memory_order_relaxed);
             const bool cheap = cam->model == ACM_UCM || cam->model == ACM_EUCM ||
-                               cam->model == ACM_FOV;
+                               cam->model == ACM_FOV || cam->model == ACM_KANNALA_BRANDT;
             const int wv = wv0 < 0 ? (cheap ? 3 : 2) : wv0;
             auto wlaunch = [&](auto kern, int spw) {
                 const size_t nwb = (nseg + 4 * (size_t)spw - 1) / (4 * (size_t)spw);
@@ -4468,14 +4530,12 @@ ACM_API size_t acm_median_workspace_size(size_t n) {
     return 2 * sizeof(SelState) + 2 * kSelBins * sizeof(double) + 16 + n * sizeof(double);
 }
 
-ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
-                                       const double* n_valid_device, uint64_t n_valid,
-                                       double* out, void* workspace, size_t workspace_bytes,
-                                       acm_allreduce_fn allreduce, void* allreduce_ctx,
-                                       void* stream) {
-    if (!out || !workspace || (n && !values)) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
-    if (workspace_bytes < acm_median_workspace_size(n))
-        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "median workspace too small");
+// hparts / hnb: pass 0's histogram already counted per workgroup by
+// k_reproj_pass1<HIST> (acm_reprojection_error): merged instead of read.
+static int median_impl(size_t n, const double* values, const double* n_valid_device,
+                       uint64_t n_valid, double* out, void* workspace,
+                       acm_allreduce_fn allreduce, void* allreduce_ctx, void* stream,
+                       const unsigned int* hparts, int hnb) {
     hipStream_t s = (hipStream_t)stream;
     SelState* st = (SelState*)workspace;
     double* hist = (double*)(st + 2);
@@ -4495,7 +4555,10 @@ ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
         if (pass == kFullPasses)
             hipLaunchKernelGGL((ntl ? k_sel_compact<true> : k_sel_compact<false>), dim3(nb),
                                dim3(kSelBlock), 0, s, n, values, st, cbuf, count);
-        if (pass == 0)
+        if (pass == 0 && hparts)
+            hipLaunchKernelGGL(k_sel_hist_merge, dim3(kSelBins / kBlock, kSelMergeG), dim3(kBlock),
+                               0, s, hparts, hnb, hist);
+        else if (pass == 0)
             hipLaunchKernelGGL((ntl ? k_sel_hist<true, true> : k_sel_hist<true, false>), dim3(nb),
                                dim3(kSelBlock), 0, s, n, nullptr, values, st, pass, hist);
         else if (pass < kFullPasses)
@@ -4516,6 +4579,52 @@ ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
     hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(64), 0, s, st, st + 1, n_valid_device,
                        (unsigned long long)n_valid, out);
     return check_launch("acm_median_valid");
+}
+
+ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
+                                       const double* n_valid_device, uint64_t n_valid,
+                                       double* out, void* workspace, size_t workspace_bytes,
+                                       acm_allreduce_fn allreduce, void* allreduce_ctx,
+                                       void* stream) {
+    if (!out || !workspace || (n && !values)) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_median_workspace_size(n))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "median workspace too small");
+    return median_impl(n, values, n_valid_device, n_valid, out, workspace, allreduce,
+                       allreduce_ctx, stream, nullptr, 0);
+}
+
+// compute_reprojection_error in one call: [errors n f64 (when the caller
+// passes none)] | reprojection partials | pass-0 histogram partials
+// (nb x 2048 u32) | median workspace
+static size_t reproj_error_hist_offset(size_t n) {
+    return (acm_reprojection_stats_workspace_size(n) + 255) / 256 * 256;
+}
+static size_t reproj_error_median_offset(size_t n) {
+    return reproj_error_hist_offset(n) +
+           ((size_t)ne_blocks(n) * kSelBins * sizeof(unsigned int) + 255) / 256 * 256;
+}
+ACM_API size_t acm_reprojection_error_workspace_size(size_t n) {
+    return reproj_error_median_offset(n) + acm_median_workspace_size(n);
+}
+
+ACM_API int acm_reprojection_error(const acm_camera* cam, size_t n, const double* points_3d,
+                                   int layout, const double* points_2d, double* result,
+                                   double* errors, void* workspace, size_t workspace_bytes,
+                                   void* stream) {
+    if (!result || !workspace || (n && (!points_3d || !points_2d)))
+        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_reprojection_error_workspace_size(n))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "reprojection-error workspace too small");
+    char* ws = (char*)workspace;
+    unsigned int* hparts = (unsigned int*)(ws + reproj_error_hist_offset(n));
+    int nb = 0;
+    int rc = reprojection_stats_impl(cam, n, points_3d, layout, points_2d, result, errors,
+                                     workspace, (hipStream_t)stream, hparts, &nb);
+    if (rc) return rc;
+    const double* errs = errors ? errors : (const double*)workspace;
+    // n_valid from result[5] on the device: no host round trip in between
+    return median_impl(n, errs, result + 5, 0, result + 8, ws + reproj_error_median_offset(n),
+                       nullptr, nullptr, stream, hparts, nb);
 }
 
 ACM_API int acm_median_valid(size_t n, const double* values, const double* n_valid_device,

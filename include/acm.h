@@ -206,6 +206,20 @@ ACM_API int acm_reprojection_stats(const acm_camera *cam, size_t n,
                                    const double *points_2d, double *result,
                                    double *errors, void *workspace,
                                    size_t workspace_bytes, void *stream);
+/* compute_reprojection_error (error_metrics.rs:62-121) in full, one call:
+ * result (device, 9 f64) = acm_reprojection_stats' 8 + [8] the median of the
+ * valid errors (acm_median_valid's rule; NaN when n_valid = 0).  The
+ * statistics pass also counts the median's first radix-select histogram
+ * (per workgroup, merged afterwards), so the median reads the errors one
+ * time fewer than acm_reprojection_stats + acm_median_valid, and n_valid
+ * stays on the device in between.  errors: nullable device N f64 output
+ * (NaN if failed); when NULL they live in the workspace. */
+ACM_API size_t acm_reprojection_error_workspace_size(size_t n);
+ACM_API int acm_reprojection_error(const acm_camera *cam, size_t n,
+                                   const double *points_3d, int layout,
+                                   const double *points_2d, double *result,
+                                   double *errors, void *workspace,
+                                   size_t workspace_bytes, void *stream);
 /* Host-side merge of the results of disjoint shards (the multi-GPU form of
  * compute_reprojection_error, error_metrics.rs:86-111): parts = nparts x 8
  * host doubles, each an acm_reprojection_stats result, folded in order --

@@ -338,6 +338,57 @@ def test_reprojection_error_zero_points():
                                         torch.tensor([[1.0, 1.0]]))
 
 
+@pytest.mark.parametrize("n", [1, 2, 1000, 2_000_003])
+def test_reprojection_error_fused_matches_two_calls(n):
+    """acm_reprojection_error (statistics + median, the median's first
+    histogram counted by the statistics pass) against acm_reprojection_stats
+    + acm_median_valid on the same inputs: the same errors and the same
+    median bit for bit, the statistics to rounding (the two passes may run
+    different workgroup counts).  Failed projections (z < 0) and NaN
+    observations are in the input; errors both into the caller's buffer and
+    into the workspace."""
+    import ctypes
+    import torch
+    from apex_camera_models import _lib, samples, util
+    L = _lib.load()
+    params, (w, h) = samples.SAMPLES[3]
+    rng = np.random.default_rng(n)
+    xyz = np.stack([rng.uniform(-1, 1, n), rng.uniform(-1, 1, n), rng.uniform(-0.3, 2.0, n)], 1)
+    obs = rng.uniform(0, w, (n, 2))
+    obs[::7] = np.nan
+    m = _model_obj(3, params, w, h)
+    p3 = torch.as_tensor(xyz, device="cuda")
+    p2 = torch.as_tensor(obs, device="cuda")
+    e_sep = torch.empty((n,), dtype=torch.float64, device="cuda")
+    st = util.reprojection_stats(m, p3, p2, e_sep)
+    nv = int(st[5].item())
+    med = util.reprojection_median(e_sep, nv) if nv else float("nan")
+    cam = m.acm_camera()
+    wsb = L.acm_reprojection_error_workspace_size(n)
+    for own_errors in (True, False):
+        ws = torch.empty(((wsb + 7) // 8,), dtype=torch.float64, device="cuda")
+        res = torch.empty((9,), dtype=torch.float64, device="cuda")
+        e = torch.full((n,), -1.0, dtype=torch.float64, device="cuda")
+        _lib.check(L.acm_reprojection_error(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
+                                            p2.data_ptr(), res.data_ptr(),
+                                            e.data_ptr() if own_errors else None, ws.data_ptr(),
+                                            wsb, torch.cuda.current_stream().cuda_stream))
+        r = res.cpu().numpy()
+        s0 = st.cpu().numpy()
+        assert r[5] == s0[5]
+        if own_errors:
+            assert torch.equal(torch.isnan(e), torch.isnan(e_sep))
+            ok = ~torch.isnan(e)
+            assert torch.equal(e[ok], e_sep[ok])
+        if nv == 0:
+            assert np.isnan(r[8])
+            continue
+        assert r[8] == med, (r[8], med)
+        assert r[1] == s0[1] and r[2] == s0[2]  # min, max
+        for k in (0, 3, 4, 6, 7):
+            assert abs(r[k] - s0[k]) <= 1e-12 * max(abs(s0[k]), 1.0), (k, r[k], s0[k])
+
+
 @pytest.mark.parametrize("n", [2, 100, 500, 20_000])
 @pytest.mark.parametrize("model", range(7))
 def test_sample_points_vs_oracle(model, n):

@@ -97,6 +97,22 @@ def lm_wall(src, xyz, uv, target, reps=5):
             "termination": res.termination}
 
 
+def warm_convert(src, xyz, uv, reps=3):
+    """conversion.convert to double_sphere (camera_converter.rs:355-488),
+    wall: one untimed call first (the caching allocator's first multi-GB
+    workspaces and the first launches), then the fastest of `reps`."""
+    import torch
+    from apex_camera_models import conversion
+    conversion.convert(src, "double_sphere", xyz, uv)
+    best, met = float("inf"), None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        met = conversion.convert(src, "double_sphere", xyz, uv)
+        best = min(best, time.perf_counter() - t0)
+    return met, best
+
+
 def config3(n_target):
     """DS residual+J and fused normal equations over ~10M KB-sampled
     correspondences, inside the bounded LM of camera_converter.rs:355-488."""
@@ -135,9 +151,7 @@ def config3(n_target):
     out = torch.empty((6 * 6 + 6 + 2,), dtype=torch.float64, device="cuda")
     ms_ne = timed(lambda: f.normal_equations(p, out))
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    met = conversion.convert(src, "double_sphere", xyz, uv)
-    t_conv = time.perf_counter() - t0
+    met, t_conv = warm_convert(src, xyz, uv)
     emit({"config": 3, **lm_wall(src, xyz, uv, "double_sphere")})
     emit({"config": 3, "what": "DS residual+J (2N x 6) kernel", "points": n,
           "ms": round(ms_rj, 4), "Mpoints_per_s": round(n / ms_rj / 1e3, 1),
@@ -145,7 +159,8 @@ def config3(n_target):
     emit({"config": 3, "what": "DS fused normal equations (JtJ, Jtr, cost)", "points": n,
           "ms": round(ms_ne, 4), "Mpoints_per_s": round(n / ms_ne / 1e3, 1),
           "GBps": round(40 * n / ms_ne / 1e6, 1)})
-    emit({"config": 3, "what": "KB->DS conversion: linear estimation + bounded LM (wall)",
+    emit({"config": 3,
+          "what": "KB->DS conversion: linear estimation + bounded LM (wall, warm, best of 3)",
           "points": n, "sample_points_s": round(t_sample, 4), "convert_s": round(t_conv, 4),
           "lm_iterations": met.lm_iterations, "termination": met.lm_termination,
           "final_mean_px": met.final_reprojection_error.mean,
@@ -302,11 +317,9 @@ def config5(n_cells):
     torch.cuda.synchronize()
     t_s = time.perf_counter() - t0
     n = xyz.shape[0]
-    t0 = time.perf_counter()
-    met = conversion.convert(src, "double_sphere", xyz, uv)
-    t_c = time.perf_counter() - t0
+    met, t_c = warm_convert(src, xyz, uv)
     emit({"config": 5, **lm_wall(src, xyz, uv, "double_sphere", reps=2)})
-    emit({"config": 5, "what": "KB->DS conversion (sample_points + linear_estimation + LM)",
+    emit({"config": 5, "what": "KB->DS conversion (sample_points; convert() wall, warm, best of 3)",
           "requested": n_cells, "correspondences": n, "sample_points_s": round(t_s, 4),
           "convert_s": round(t_c, 4), "lm_iterations": met.lm_iterations,
           "termination": met.lm_termination,

@@ -72,7 +72,7 @@ def main():
                                            xyz.data_ptr(), cnt.data_ptr(), ws.data_ptr(), wsb,
                                            sh))
         cells = {}
-        for _ in range(3):
+        for _ in range(int(os.environ.get("REPS", "3"))):
             for v in VS:
                 call(v)
                 torch.cuda.synchronize()

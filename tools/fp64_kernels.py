@@ -21,7 +21,8 @@ sys.path.insert(0, ROOT)
 ALL = ("radtan_unproject", "kb_unproject", "kb_normal_eq", "fov_grid", "sample_kb")
 # also selectable with --only: "ds_ne9" / "ds_ne93", the DS fused normal
 # equations on the config-3 (9.29M) / config-5 (92.9M) KB-sampled
-# correspondences at the DS linear estimate (the LM's inner loop)
+# correspondences at the DS linear estimate (the LM's inner loop);
+# "ds_reproj9" / "ds_reproj93", compute_reprojection_error on the same data
 
 
 def main():
@@ -100,18 +101,24 @@ def main():
         ms = timed(lambda: fov.linear_estimation(sxyz, suv))
         emit("fov_grid", sxyz.shape[0], ms, 40, evaluations=290 * sxyz.shape[0])
         del suv, sxyz
-    for tag, cells in (("ds_ne9", 10_000_000), ("ds_ne93", 100_000_000)):
-        if tag not in want:
+    for tag, rtag, cells in (("ds_ne9", "ds_reproj9", 10_000_000),
+                             ("ds_ne93", "ds_reproj93", 100_000_000)):
+        if tag not in want and rtag not in want:
             continue
         suv, sxyz = util.sample_points(src, cells)
         ds = conversion._init_target("double_sphere", src)
         ds.linear_estimation(sxyz, suv)
-        f = factors.DoubleSphereCameraParamsFactor(sxyz, suv, Resolution(kw, kh))
-        out = torch.empty((6 * 6 + 6 + 2,), dtype=torch.float64, device="cuda")
-        p = ds.params()
-        ms = timed(lambda: f.normal_equations(p, out))
-        emit(tag, sxyz.shape[0], ms, 40)
-        del suv, sxyz, f
+        if tag in want:
+            f = factors.DoubleSphereCameraParamsFactor(sxyz, suv, Resolution(kw, kh))
+            out = torch.empty((6 * 6 + 6 + 2,), dtype=torch.float64, device="cuda")
+            p = ds.params()
+            ms = timed(lambda: f.normal_equations(p, out))
+            emit(tag, sxyz.shape[0], ms, 40)
+            del f
+        if rtag in want:  # compute_reprojection_error (reads 40 B, writes 8 B per point)
+            ms = timed(lambda: util.compute_reprojection_error(ds, sxyz, suv))
+            emit(rtag, sxyz.shape[0], ms, 48)
+        del suv, sxyz
     if "sample_kb" in want:
         if a.sample_fused is not None:
             L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, a.sample_fused)

@@ -176,3 +176,73 @@ int acm_probe_mimic(size_t n, const double* xyz, double* uv, uint8_t* st, double
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// acm_probe_write_sample: the store ceiling of the sample_points write pass
+//  -- write-only kernels in its output shape (a 16-B pixel
+// stream and a 24-B ray stream per kept point, 3.72 GB at config 5), no loads
+// and no arithmetic; driven by tools/diag_store.py.
+namespace {
+
+// variant 0: one 16-B store per lane per stream, grid-stride over points
+// (uv: point i -> 16 B at 16 i; rays: 24 B at 24 i as 3 x 8 B)
+__global__ __launch_bounds__(256) void k_store_aos(double2* __restrict__ uv,
+                                                   double* __restrict__ xyz, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uv[i] = make_double2((double)i, 1.0);
+        xyz[3 * i + 0] = 0.5;
+        xyz[3 * i + 1] = 0.25;
+        xyz[3 * i + 2] = 1.0;
+    }
+}
+
+// variant 1: both streams as flat 16-B vectors (uv: 1 per point, rays: 1.5
+// per point), every lane one dwordx4 per step -- the best case for the
+// store unit
+__global__ __launch_bounds__(256) void k_store_v4(double2* __restrict__ a, uint64_t na,
+                                                  double2* __restrict__ b, uint64_t nb) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const double2 v = make_double2(1.0, 2.0);
+    for (uint64_t i = t; i < na; i += stride) a[i] = v;
+    for (uint64_t i = t; i < nb; i += stride) b[i] = v;
+}
+
+// variant 2: like 1 but each wave writes a contiguous 64 x 16 B run per
+// step from a per-wave chunk (the write pass's "one contiguous run per wave")
+__global__ __launch_bounds__(256) void k_store_runs(double2* __restrict__ a, uint64_t na,
+                                                    double2* __restrict__ b, uint64_t nb,
+                                                    uint64_t chunk) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const unsigned lane = threadIdx.x & 63;
+    const double2 v = make_double2(1.0, 2.0);
+    uint64_t lo = wave * chunk, hi = lo + chunk;
+    for (uint64_t i = lo + lane; i < hi && i < na; i += 64) a[i] = v;
+    lo = wave * chunk * 3 / 2;
+    hi = lo + chunk * 3 / 2;
+    for (uint64_t i = lo + lane; i < hi && i < nb; i += 64) b[i] = v;
+}
+
+}  // namespace
+
+extern "C" int acm_probe_write_sample(int variant, void* uv, void* xyz, uint64_t n, int blocks,
+                           uint64_t chunk, hipStream_t s) {
+    switch (variant) {
+    case 0:
+        hipLaunchKernelGGL(k_store_aos, dim3(blocks), dim3(256), 0, s, (double2*)uv,
+                           (double*)xyz, n);
+        break;
+    case 1:
+        hipLaunchKernelGGL(k_store_v4, dim3(blocks), dim3(256), 0, s, (double2*)uv, n,
+                           (double2*)xyz, n * 3 / 2);
+        break;
+    case 2:
+        hipLaunchKernelGGL(k_store_runs, dim3(blocks), dim3(256), 0, s, (double2*)uv, n,
+                           (double2*)xyz, n * 3 / 2, chunk);
+        break;
+    default:
+        return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
