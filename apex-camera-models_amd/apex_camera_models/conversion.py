@@ -72,9 +72,12 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
         estimate = lambda m: D.distributed_linear_estimation(m, points_3d, points_2d, group)  # noqa: E731
     else:
         reproj = lambda m: util.compute_reprojection_error(m, points_3d, points_2d)  # noqa: E731
-        estimate = lambda m: m.linear_estimation(points_3d, points_2d)  # noqa: E731
-    initial = reproj(model)
-    estimate(model)
+    if allreduce is None:
+        # the initial error and the linear estimation in one pass (r04)
+        initial = util.initial_error_and_linear_estimation(model, points_3d, points_2d)
+    else:
+        initial = reproj(model)
+        estimate(model)
     cfg = config or LevenbergMarquardtConfig()
     status = "Converged"
     res = None

@@ -12,7 +12,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from .camera import CameraModel, _as_device_f64, _stream_handle
+from .camera import CameraModel, InvalidParams, NumericalError, _as_device_f64, _stream_handle
 
 
 class UtilError(Exception):
@@ -101,6 +101,42 @@ def compute_reprojection_error(camera_model: CameraModel, points3d, points2d) ->
     n_valid = int(out[5])
     if n_valid == 0:
         raise ZeroProjectionPoints()
+    return ProjectionError(rmse=out[0], min=out[1], max=out[2], mean=out[3], stddev=out[4],
+                           median=out[8], n_valid=n_valid)
+
+
+def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d) -> ProjectionError:
+    """convert_to_*'s opening (camera_converter.rs:371-375): the reprojection
+    error of `model` as given, then `model.linear_estimation` -- for the TSQR
+    models one pass over the correspondences (acm_linear_estimation_with_error).
+    Raises like the two calls in that order: ZeroProjectionPoints first, then
+    the estimation's InvalidParams / NumericalError."""
+    L = _lib.load()
+    p3 = _as_device_f64(points3d, 3)
+    p2 = _as_device_f64(points2d, 2)
+    n = p3.shape[0]
+    if p2.shape[0] != n:
+        raise ValueError("points3d and points2d must have the same number of columns")
+    ws_bytes = L.acm_linear_estimation_with_error_workspace_size(model.MODEL_ID, n)
+    if ws_bytes == 0:
+        raise InvalidParams(f"{model.NAME} has no GPU linear_estimation")
+    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=p3.device)
+    res = torch.empty((9,), dtype=torch.float64, device=p3.device)
+    cam = model.acm_camera()
+    rc = L.acm_linear_estimation_with_error(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
+                                            p2.data_ptr(), res.data_ptr(), ws.data_ptr(),
+                                            ws_bytes, _stream_handle())
+    if rc not in (_lib.ACM_SUCCESS, _lib.ERR_INVALID_PARAMS, _lib.ERR_NUMERICAL):
+        _lib.check(rc)
+    out = res.cpu().tolist()
+    n_valid = int(out[5])
+    if n_valid == 0:
+        raise ZeroProjectionPoints()
+    if rc == _lib.ERR_INVALID_PARAMS:
+        raise InvalidParams(_lib.last_error())
+    if rc == _lib.ERR_NUMERICAL:
+        raise NumericalError(_lib.last_error())
+    model._set_params(list(cam.params)[: model.NUM_PARAMS])
     return ProjectionError(rmse=out[0], min=out[1], max=out[2], mean=out[3], stddev=out[4],
                            median=out[8], n_valid=n_valid)
 

@@ -1238,7 +1238,6 @@ __device__ __forceinline__ Mv mv_wave(Mv a) {
     return a;
 }
 
-constexpr int kReprojU = 2;
 constexpr int kReprojW = 7;  // per-workgroup [sum e, sum e^2, min, max, count, mean, M2]
 
 // [sum, sumsq, min, max, count] + (count, mean, M2) of a wave -> lane 0's
@@ -1299,14 +1298,66 @@ __device__ __forceinline__ void sel_count(unsigned int* h, bool pred, unsigned d
 // e_i = ||proj(p_i) - uv_i|| (NaN if the projection fails); per-workgroup
 // partials (kReprojW doubles).  NTS: non-temporal error stores.  Software
 // pipelined like k_normal_eq (r04): one point per lane step, the loads of the
-// next kReprojA steps in flight in static slots, branch-free (past the end:
-// point n - 1 again, never used) -- 2 points per lane per chunk without
-// prefetch ran 4.96 TB/s at 92.9M (profiles/r04j_convert_kernel_stats.csv).
+// next kReprojA = 6 steps in flight in static slots, branch-free (past the
+// end: point n - 1 again, never used).  compute_reprojection_error at 92.9M
+// (profiles/r04m_*, r04n_*, same box, interleaved): 2 slots 1.271 ms, 4
+// slots 1.198 / 1.203, 6 slots 1.179, 8 slots 1.179 (126 VGPRs); each
+// workgroup streaming one contiguous range instead of the grid stride
+// 1.251 (2 slots) / 1.269 (4 slots); plain instead of non-temporal error
+// stores 1.287.  The round-3 form (2 points per lane per chunk, no
+// prefetch) ran the pass at 4.96 TB/s (profiles/r04j_convert_kernel_stats.csv).
 // HIST (acm_reprojection_error): the median's first radix-select histogram
 // (the 11-bit digit of bits 53..63 of every error, NaN included, exactly
 // k_sel_hist's pass 0) is counted here in LDS and written per workgroup to
 // hparts (2048 u32), which saves the median one full read of the errors.
-constexpr int kReprojA = 2;
+constexpr int kReprojA = 6;
+
+// One lane's reprojection statistics: [sum, sumsq, min, max, count] and the
+// shifted sums about its first valid error (see the comment above Mv).
+struct ReprojAcc {
+    double s = 0.0, ss = 0.0, mn = INFINITY, mx = -INFINITY, cnt = 0.0;
+    double K = 0.0, S = 0.0, Q = 0.0;
+    // One validity rule for the statistics and the median: an Ok projection
+    // whose error is NaN (a NaN observation) is not a valid error --
+    // acm_median_valid skips NaN too.  (The reference would sum the NaN and
+    // then panic in its median sort, error_metrics.rs:104-108
+    // partial_cmp().unwrap().)
+    __device__ __forceinline__ void add(double e) {
+        if (e == e) {
+            s += e;
+            ss += e * e;
+            mn = fmin(mn, e);
+            mx = fmax(mx, e);
+            K = cnt == 0.0 ? e : K;
+            const double d = e - K;
+            S += d;
+            Q += d * d;
+            cnt += 1.0;
+        }
+    }
+    // workgroup partials (kReprojW doubles); every lane of the workgroup calls it
+    __device__ __forceinline__ void store(double* __restrict__ out) const {
+        const double mloc = cnt > 0.0 ? S / cnt : 0.0;
+        const Mv v{cnt, K + mloc, cnt > 0.0 ? Q - S * mloc : 0.0};
+        reproj_block_store(s, ss, mn, mx, v, out);
+    }
+};
+
+// e = ||proj(p) - o||, NaN if the projection fails (error_metrics.rs:70-84)
+template <class M>
+__device__ __forceinline__ double reproj_error(const Cam<double>& c, double x, double y, double z,
+                                               double2 o) {
+    double u, v;
+    const uint8_t st = M::template project<false>(c, x, y, z, u, v, nullptr, nullptr);
+    if (st != ST_OK) return __builtin_nan("");
+    const double du = u - o.x, dv = v - o.y;
+    return sqrt(du * du + dv * dv);
+}
+
+// the median's pass-0 digit of an error (bits 53..63, k_sel_hist's pass 0)
+__device__ __forceinline__ unsigned sel_digit0(double e) {
+    return (unsigned)(((unsigned long long)__double_as_longlong(e) >> 53) & (kSelBins - 1));
+}
 
 template <class TagT, int LAYOUT, bool NTL, bool NTS, bool HIST>
 __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t n,
@@ -1323,8 +1374,7 @@ __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t 
         __syncthreads();
     }
     const Cam<double> c = make_cam<double>(cam);
-    double s = 0.0, ss = 0.0, mn = INFINITY, mx = -INFINITY, cnt = 0.0;
-    double K = 0.0, S = 0.0, Q = 0.0;  // shifted sums about this lane's first valid error
+    ReprojAcc acc;
     const size_t stride = (size_t)gridDim.x * kBlock;
     size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
     constexpr int A = kReprojA;
@@ -1346,40 +1396,16 @@ __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t 
             const bool in = iq < n;
             double e = __builtin_nan("");
             if (in) {
-                double u, v;
-                const uint8_t st = M::template project<false>(c, xs[q], ys[q], zs[q], u, v,
-                                                              nullptr, nullptr);
-                if (st == ST_OK) {
-                    const double du = u - os[q].x, dv = v - os[q].y;
-                    e = sqrt(du * du + dv * dv);
-                }
-                // One validity rule for the statistics and the median: an Ok
-                // projection whose error is NaN (a NaN observation) is not a
-                // valid error -- acm_median_valid skips NaN too.  (The
-                // reference would sum the NaN and then panic in its median
-                // sort, error_metrics.rs:104-108 partial_cmp().unwrap().)
-                if (e == e) {
-                    s += e;
-                    ss += e * e;
-                    mn = fmin(mn, e);
-                    mx = fmax(mx, e);
-                    K = cnt == 0.0 ? e : K;
-                    const double d = e - K;
-                    S += d;
-                    Q += d * d;
-                    cnt += 1.0;
-                }
+                e = reproj_error<M>(c, xs[q], ys[q], zs[q], os[q]);
+                acc.add(e);
                 if (NTS) __builtin_nontemporal_store(e, errs + iq);
                 else errs[iq] = e;
             }
-            if constexpr (HIST)
-                sel_count<true>(h, in, (unsigned)(((unsigned long long)__double_as_longlong(e) >> 53) & (HB - 1)));
+            if constexpr (HIST) sel_count<true>(h, in, sel_digit0(e));
             load_slot(q, iq + (size_t)A * stride);
         }
     }
-    const double mloc = cnt > 0.0 ? S / cnt : 0.0;
-    const Mv v{cnt, K + mloc, cnt > 0.0 ? Q - S * mloc : 0.0};
-    reproj_block_store(s, ss, mn, mx, v, parts + (size_t)blockIdx.x * kReprojW);
+    acc.store(parts + (size_t)blockIdx.x * kReprojW);
     if constexpr (HIST) {
         __syncthreads();
         unsigned int* hp = hparts + (size_t)blockIdx.x * HB;
@@ -2598,6 +2624,42 @@ __device__ __forceinline__ void tri_add_row(double (&R)[Tri<M>::S], double (&row
     }
 }
 
+// fold NR rows at once into R with one Householder reflection per column
+// (r04): the stacked [R; rows] has, in column j, R's diagonal x0 above the
+// rows' entries; the reflector that zeroes the rows' column j costs one
+// square root and one division for all NR rows, where tri_add_row's Givens
+// rotations take one of each per row and column.  Backward stable like the
+// rotations; the diagonal is kept >= 0 (a row of R may be negated: R^T R and
+// the solve of [A | b] are unchanged), as tri_add_row's is.
+template <int M, int NR>
+__device__ __forceinline__ void tri_add_rows(double (&R)[Tri<M>::S], double (&rows)[NR][M]) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        double sig = 0.0;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) sig += rows[i][j] * rows[i][j];
+        if (sig != 0.0) {
+            const double x0 = R[Tri<M>::at(j, j)];
+            const double nrm = sqrt(x0 * x0 + sig);
+            const double v0 = x0 >= 0.0 ? x0 + nrm : x0 - nrm;  // no cancellation
+            const double beta = 2.0 / (v0 * v0 + sig);
+            // new diagonal -sign(x0) nrm, flipped to +nrm with its row
+            const double flip = x0 >= 0.0 ? -1.0 : 1.0;
+            R[Tri<M>::at(j, j)] = nrm;
+#pragma unroll
+            for (int l = j + 1; l < M; ++l) {
+                double d = v0 * R[Tri<M>::at(j, l)];
+#pragma unroll
+                for (int i = 0; i < NR; ++i) d += rows[i][j] * rows[i][l];
+                const double t = beta * d;
+                R[Tri<M>::at(j, l)] = flip * (R[Tri<M>::at(j, l)] - t * v0);
+#pragma unroll
+                for (int i = 0; i < NR; ++i) rows[i][l] -= t * rows[i][j];
+            }
+        }
+    }
+}
+
 template <int M>
 __device__ __forceinline__ void tri_merge(double (&R)[Tri<M>::S], const double (&O)[Tri<M>::S]) {
 #pragma unroll
@@ -2670,31 +2732,82 @@ struct LinRows<ACM_RADTAN> {  // rad_tan.rs:168-198, k = 3
 };
 
 constexpr int kTsqrMaxBlocks = 2048;
+template <int M> constexpr int kTsqrB = M <= 3 ? 4 : 2;
 
-template <int MODEL, int LAYOUT>
+// TagR != void (acm_linear_estimation_with_error, r04): the same pass also
+// computes the reprojection error of the camera as given -- the reference's
+// initial_error, computed just before linear_estimation on the same
+// correspondences (camera_converter.rs:371-375) -- so the 40 B per point are
+// read once for both: per-point errors (errs), k_reproj_pass1's statistics
+// partials (rparts) and the median's pass-0 histogram (hparts).
+template <int MODEL, int LAYOUT, class TagR = void, bool NTS = false>
 __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
                                                  const double* __restrict__ pts,
                                                  const double* __restrict__ obs,
                                                  double* __restrict__ parts,
-                                                 int* __restrict__ err_flag) {
+                                                 int* __restrict__ err_flag,
+                                                 double* __restrict__ errs,
+                                                 double* __restrict__ rparts,
+                                                 unsigned int* __restrict__ hparts) {
     using RW = LinRows<MODEL>;
     constexpr int M = RW::K + 1;
     constexpr int S = Tri<M>::S;
+    constexpr bool REPROJ = !std::is_void<TagR>::value;
+    __shared__ unsigned int h[REPROJ ? kSelBins : 1];
+    if constexpr (REPROJ) {
+        for (int j = threadIdx.x; j < kSelBins; j += kBlock) h[j] = 0;
+        __syncthreads();
+    }
+    ReprojAcc acc;
     const Cam<double> c = make_cam<double>(cam);
     double R[S];
 #pragma unroll
     for (int q = 0; q < S; ++q) R[q] = 0.0;
     int err = 0;
     const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        double x, y, z;
-        load_point<LAYOUT>(pts, n, i, x, y, z);
-        const double2 o = *reinterpret_cast<const double2*>(obs + 2 * i);
-        double r0[M], r1[M];
-        if (RW::rows(c, x, y, z, o.x, o.y, r0, r1, err)) {
-            tri_add_row<M>(R, r0);
-            tri_add_row<M>(R, r1);
+    // kTsqrB<M> points per lane step (their loads in flight together), their
+    // 2 kTsqrB rows folded in with one Householder reflection per column
+    constexpr int B = kTsqrB<M>;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)B * stride) {
+        double x[B], y[B], z[B];
+        double2 o[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const size_t ib = i + (size_t)b * stride;
+            const size_t ic = ib < n ? ib : n - 1;
+            load_point<LAYOUT>(pts, n, ic, x[b], y[b], z[b]);
+            o[b] = *reinterpret_cast<const double2*>(obs + 2 * ic);
         }
+        if constexpr (REPROJ) {
+            using MR = typename TagR::template type<double>;
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const size_t ib = i + (size_t)b * stride;
+                const bool in = ib < n;
+                double e = __builtin_nan("");
+                if (in) {
+                    e = reproj_error<MR>(c, x[b], y[b], z[b], o[b]);
+                    acc.add(e);
+                    if (NTS) __builtin_nontemporal_store(e, errs + ib);
+                    else errs[ib] = e;
+                }
+                sel_count<true>(h, in, sel_digit0(e));
+            }
+        }
+        double rows[2 * B][M];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const bool in = i + (size_t)b * stride < n;
+            int e = 0;
+            const bool ok = in && RW::rows(c, x[b], y[b], z[b], o[b].x, o[b].y, rows[2 * b],
+                                           rows[2 * b + 1], e);
+            if (in) err |= e;
+            if (!ok) {
+#pragma unroll
+                for (int q = 0; q < M; ++q) rows[2 * b][q] = rows[2 * b + 1][q] = 0.0;
+            }
+        }
+        tri_add_rows<M, 2 * B>(R, rows);
     }
     // wave merge (fixed butterfly order)
 #pragma unroll
@@ -2724,6 +2837,12 @@ __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
 #pragma unroll
         for (int q = 0; q < S; ++q) parts[(size_t)blockIdx.x * S + q] = R[q];
         if (serr) atomicOr(err_flag, 1);
+    }
+    if constexpr (REPROJ) {
+        acc.store(rparts + (size_t)blockIdx.x * kReprojW);
+        __syncthreads();
+        unsigned int* hp = hparts + (size_t)blockIdx.x * kSelBins;
+        for (int j = threadIdx.x; j < kSelBins; j += kBlock) hp[j] = h[j];
     }
 }
 
@@ -4409,7 +4528,7 @@ ACM_API int acm_linear_system_qr(const acm_camera* cam, size_t n, const double* 
         const int nb = std::min((int)tsqr_blocks(n),
                                 resident_blocks(reinterpret_cast<const void*>(kern)));
         hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
-                           points_2d, parts, error_flag);
+                           points_2d, parts, error_flag, nullptr, nullptr, nullptr);
         hipLaunchKernelGGL((k_tsqr_final<M>), dim3(1), dim3(kBlock), 0, s, parts, nb, r_factor);
     };
     switch (cam->model) {
@@ -4420,6 +4539,69 @@ ACM_API int acm_linear_system_qr(const acm_camera* cam, size_t n, const double* 
     default: go(std::integral_constant<int, ACM_EUCM>{}); break;
     }
     return check_launch("acm_linear_system_qr");
+}
+
+static size_t reproj_error_hist_offset(size_t n);
+static size_t reproj_error_median_offset(size_t n);
+static int median_impl(size_t n, const double* values, const double* n_valid_device,
+                       uint64_t n_valid, double* out, void* workspace,
+                       acm_allreduce_fn allreduce, void* allreduce_ctx, void* stream,
+                       const unsigned int* hparts, int hnb);
+
+extern "C++" {
+namespace acm {
+// acm_linear_estimation_with_error's device half (solver.hip): one pass of
+// k_tsqr<MOD, LAYOUT, TagR> builds the R factor of [A | b] and the
+// reprojection error of *cam as given, then the factor merge, the error
+// statistics and the median follow on the stream.  ws_err is laid out as
+// acm_reprojection_error's workspace (errors first); result: its 9 f64.
+int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
+                           const double* points_2d, double* r_factor, int* error_flag,
+                           double* result, void* ws_qr, void* ws_err, void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if ((rc = check_layout(layout))) return rc;
+    if (acm_linear_system_columns(cam->model) < 0)
+        return fail(ACM_ERR_NOT_SUPPORTED, "model has no linear_estimation");
+    hipStream_t s = (hipStream_t)stream;
+    double* parts = (double*)ws_qr;
+    double* errs = (double*)ws_err;
+    double* p1 = errs + n;
+    double* tot = p1 + (size_t)ne_blocks(n) * kReprojW;
+    unsigned int* hparts = (unsigned int*)((char*)ws_err + reproj_error_hist_offset(n));
+    if (hipMemsetAsync(error_flag, 0, sizeof(int), s) != hipSuccess)
+        return check_launch("acm_linear_estimation_with_error (memset)");
+    int nb = 1;
+    auto go = [&](auto model_c, auto tag) {
+        constexpr int MOD = decltype(model_c)::value;
+        using TagR = decltype(tag);
+        constexpr int M = LinRows<MOD>::K + 1;
+        auto kern = layout == ACM_LAYOUT_AOS ? k_tsqr<MOD, ACM_LAYOUT_AOS, TagR, true>
+                                             : k_tsqr<MOD, ACM_LAYOUT_SOA, TagR, true>;
+        nb = std::min((int)tsqr_blocks(n), resident_blocks(reinterpret_cast<const void*>(kern)));
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
+                           points_2d, parts, error_flag, errs, p1, hparts);
+        hipLaunchKernelGGL((k_tsqr_final<M>), dim3(1), dim3(kBlock), 0, s, parts, nb, r_factor);
+    };
+    switch (cam->model) {
+    case ACM_KANNALA_BRANDT:
+        go(std::integral_constant<int, ACM_KANNALA_BRANDT>{}, Tag<KannalaBrandt>{});
+        break;
+    case ACM_RADTAN: go(std::integral_constant<int, ACM_RADTAN>{}, Tag<RadTan>{}); break;
+    case ACM_DOUBLE_SPHERE:
+        go(std::integral_constant<int, ACM_DOUBLE_SPHERE>{}, Tag<DoubleSphere>{});
+        break;
+    case ACM_UCM: go(std::integral_constant<int, ACM_UCM>{}, Tag<Ucm>{}); break;
+    default: go(std::integral_constant<int, ACM_EUCM>{}, Tag<Eucm>{}); break;
+    }
+    hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb, tot);
+    hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, result);
+    if ((rc = check_launch("acm_linear_estimation_with_error"))) return rc;
+    return median_impl(n, errs, result + 5, 0, result + 8,
+                       (char*)ws_err + reproj_error_median_offset(n), nullptr, nullptr, stream,
+                       hparts, nb);
+}
+}  // namespace acm
 }
 
 // FOV linear_estimation grid (fov.rs:153-251); the selection is host code

@@ -34,6 +34,9 @@ int lm_device();                                   // acm.hip, ACM_TUNE_LM_DEVIC
 int lm_step_launch(int P, lm::State* st, const acm_lm_config& cfg, const double* res,
                    double* dparams, int* ddone, unsigned long long* hflag,
                    unsigned long long seq, void* stream);
+int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
+                           const double* points_2d, double* r_factor, int* error_flag,
+                           double* result, void* ws_qr, void* ws_err, void* stream);
 }
 
 namespace {
@@ -264,6 +267,60 @@ ACM_API int acm_linear_estimation(acm_camera* cam, size_t n, const double* point
     int* d_err = (int*)(d_r + 16);
     rc = acm_linear_system_qr(cam, n, points_3d, layout, points_2d, d_r, d_err, workspace, qr,
                               stream);
+    if (rc) return rc;
+    double R[16];
+    int err = 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (hip_ok(hipMemcpyAsync(R, d_r, S * sizeof(double), hipMemcpyDeviceToHost, s)) ||
+        hip_ok(hipMemcpyAsync(&err, d_err, sizeof(int), hipMemcpyDeviceToHost, s)) ||
+        hip_ok(hipStreamSynchronize(s)))
+        return sfail(ACM_ERR_HIP, "linear estimation: device copy failed");
+    return acm_linear_estimation_solve(cam, n, R, err);
+}
+
+// convert_to_*'s initial_error + linear_estimation (camera_converter.rs:
+// 371-375, :507-511, ...) in one pass over the correspondences.  Workspace:
+// [TSQR partials | R + flag (32 f64) | acm_reprojection_error's workspace].
+static size_t lin_err_qr_bytes(int model, size_t n) {
+    return (acm_linear_system_qr_workspace_size(model, n) + 255) / 256 * 256;
+}
+
+ACM_API size_t acm_linear_estimation_with_error_workspace_size(int model, size_t n) {
+    const size_t le = acm_linear_estimation_workspace_size(model, n);
+    if (!le) return 0;
+    const size_t err = acm_reprojection_error_workspace_size(n);
+    if (model == ACM_FOV) return std::max(le, err);
+    return lin_err_qr_bytes(model, n) + 32 * sizeof(double) + err;
+}
+
+ACM_API int acm_linear_estimation_with_error(acm_camera* cam, size_t n, const double* points_3d,
+                                             int layout, const double* points_2d,
+                                             double* initial_error, void* workspace,
+                                             size_t workspace_bytes, void* stream) {
+    if (!cam) return sfail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
+    if (!initial_error) return sfail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    const size_t need = acm_linear_estimation_with_error_workspace_size(cam->model, n);
+    if (!need) return sfail(ACM_ERR_NOT_SUPPORTED, "model has no linear_estimation");
+    if (!workspace || workspace_bytes < need)
+        return sfail(ACM_ERR_WORKSPACE_TOO_SMALL, "linear-estimation workspace too small");
+    const int k = acm_linear_system_columns(cam->model);
+    // the reference computes initial_error first: it is written whatever the
+    // estimation then does (FOV, or too few points: the two calls in order)
+    if (k < 0 || count_check(cam->model, n) != ACM_SUCCESS) {
+        int rc = acm_reprojection_error(cam, n, points_3d, layout, points_2d, initial_error,
+                                        nullptr, workspace,
+                                        acm_reprojection_error_workspace_size(n), stream);
+        if (rc) return rc;
+        return acm_linear_estimation(cam, n, points_3d, layout, points_2d, workspace,
+                                     workspace_bytes, stream);
+    }
+    const int M = k + 1, S = M * (M + 1) / 2;
+    const size_t qr = lin_err_qr_bytes(cam->model, n);
+    double* d_r = (double*)((char*)workspace + qr);
+    int* d_err = (int*)(d_r + 16);
+    void* ws_err = (char*)workspace + qr + 32 * sizeof(double);
+    int rc = acm::linear_system_qr_error(cam, n, points_3d, layout, points_2d, d_r, d_err,
+                                         initial_error, workspace, ws_err, stream);
     if (rc) return rc;
     double R[16];
     int err = 0;

@@ -258,6 +258,20 @@ ACM_API int acm_linear_system_qr(const acm_camera *cam, size_t n,
                                  int *error_flag, void *workspace,
                                  size_t workspace_bytes, void *stream);
 ACM_API size_t acm_linear_estimation_workspace_size(int model, size_t n);
+/* convert_to_*'s opening (camera_converter.rs:371-375): the reprojection
+ * error of *cam as given (initial_error; device, 9 f64 as
+ * acm_reprojection_error) and then linear_estimation of *cam (updated in
+ * place, return code as acm_linear_estimation) -- for the TSQR models in ONE
+ * pass over the correspondences (k_tsqr also computes the errors, their
+ * statistics and the median's first histogram).  The initial error is
+ * written even when the estimation then fails (as the reference computes it
+ * first); for FOV and too-few-point calls the two run one after the other. */
+ACM_API size_t acm_linear_estimation_with_error_workspace_size(int model, size_t n);
+ACM_API int acm_linear_estimation_with_error(acm_camera *cam, size_t n,
+                                             const double *points_3d, int layout,
+                                             const double *points_2d,
+                                             double *initial_error, void *workspace,
+                                             size_t workspace_bytes, void *stream);
 /* Multi-GPU linear_estimation: each rank runs acm_linear_system_qr on its
  * shard, the packed factors (host copies) are folded in rank order with
  * acm_linear_system_r_merge (Givens; R of the stacked rows), error flags

@@ -463,3 +463,46 @@ def test_validate_conversion_accuracy_matches_oracle(target):
     assert v.status in ("EXCELLENT", "GOOD", "NEEDS IMPROVEMENT")
     if target == "double_sphere":
         assert v.status in ("EXCELLENT", "GOOD")
+
+
+@pytest.mark.parametrize("target,src", [(DS, KB), (UCM, KB), (EUCM, KB), (KB, DS), (RADTAN, KB),
+                                        (FOV, KB)])
+def test_initial_error_and_linear_estimation_fused(target, src):
+    """acm_linear_estimation_with_error (convert_to_*'s initial_error +
+    linear_estimation in one pass) against the two calls: the same errors'
+    median and extrema bit for bit, the sums to rounding, and the same
+    estimate (the fused pass may run another workgroup count, so R -- and
+    the solved parameters -- to rounding)."""
+    import torch
+    from apex_camera_models import util
+    uv, xyz, w, h = _sampled(src, 300_000)
+    sp, _ = SAMPLES[src]
+    init = {KB: sp[:4] + [0.0] * 4, DS: sp[:4] + [0.5, 0.1], UCM: sp[:4] + [0.5],
+            EUCM: sp[:4] + [0.5, 1.0], RADTAN: sp[:4] + [0.0] * 5, FOV: sp[:4] + [1.0]}[target]
+    p3, p2 = torch.as_tensor(xyz, device="cuda"), torch.as_tensor(uv, device="cuda")
+    a, b = _model(target, init, w, h), _model(target, init, w, h)
+    e0 = util.compute_reprojection_error(a, p3, p2)
+    a.linear_estimation(p3, p2)
+    e1 = util.initial_error_and_linear_estimation(b, p3, p2)
+    assert e1.n_valid == e0.n_valid
+    assert e1.median == e0.median and e1.min == e0.min and e1.max == e0.max
+    for k in ("rmse", "mean", "stddev"):
+        assert abs(getattr(e1, k) - getattr(e0, k)) <= 1e-12 * abs(getattr(e0, k)), k
+    np.testing.assert_allclose(b.params(), a.params(), rtol=1e-11, atol=1e-13)
+
+
+def test_initial_error_and_linear_estimation_errors():
+    """The reference's order: compute_reprojection_error raises first
+    (ZeroProjectionPoints), then linear_estimation (too few points)."""
+    import torch
+    from apex_camera_models import util
+    from apex_camera_models.camera import InvalidParams
+    sp, (w, h) = SAMPLES[KB]
+    m = _model(KB, sp[:4] + [0.0] * 4, w, h)
+    with pytest.raises(util.ZeroProjectionPoints):
+        util.initial_error_and_linear_estimation(m, torch.tensor([[0.1, 0.2, -1.0]] * 5),
+                                                 torch.tensor([[1.0, 1.0]] * 5))
+    uv, xyz, _, _ = _sampled(KB, 2000)
+    with pytest.raises(InvalidParams):
+        util.initial_error_and_linear_estimation(m, torch.as_tensor(xyz[:3]),
+                                                 torch.as_tensor(uv[:3]))
