@@ -501,8 +501,9 @@ ACM_API int acm_stream_synchronize(void *stream);
  * (-1 = auto = on; 0 = every segment counted cell by cell).  Same outputs.
  * ACM_TUNE_SAMPLE_WRITE: the segment path's write pass, segments per wave
  * and their order (-1 = auto = 16 interleaved across the workgroup's four
- * waves, 4 for UCM / EUCM / FOV; 1 = 64 contiguous, 2 = 16 interleaved, 3 = 4 interleaved, 4 = 16
- * contiguous, 5 = 16 interleaved with non-temporal stores).  Same outputs.
+ * waves, 4 for KB / UCM / EUCM / FOV; 1 = 64 contiguous, 2 = 16
+ * interleaved, 3 = 4 interleaved, 4 = 16 contiguous, 5 = 16 interleaved
+ * with non-temporal stores).  Same outputs.
  * ACM_TUNE_UNPROJECT_RCP: unprojections (acm_unproject, acm_sample_points*)
  * divide by fx, fy through the host's correctly rounded 1/fx, 1/fy and one
  * FMA correction, bit-identical to the division (-1 = auto = on, 0 = plain
