@@ -22,7 +22,8 @@ ALL = ("radtan_unproject", "kb_unproject", "kb_normal_eq", "fov_grid", "sample_k
 # also selectable with --only: "ds_ne9" / "ds_ne93", the DS fused normal
 # equations on the config-3 (9.29M) / config-5 (92.9M) KB-sampled
 # correspondences at the DS linear estimate (the LM's inner loop);
-# "ds_reproj9" / "ds_reproj93", compute_reprojection_error on the same data
+# "ds_reproj9" / "ds_reproj93", compute_reprojection_error on the same data;
+# "ds_prologue9" / "ds_prologue93", the initial error + linear estimation
 
 
 def main():
@@ -101,11 +102,15 @@ def main():
         ms = timed(lambda: fov.linear_estimation(sxyz, suv))
         emit("fov_grid", sxyz.shape[0], ms, 40, evaluations=290 * sxyz.shape[0])
         del suv, sxyz
-    for tag, rtag, cells in (("ds_ne9", "ds_reproj9", 10_000_000),
-                             ("ds_ne93", "ds_reproj93", 100_000_000)):
-        if tag not in want and rtag not in want:
+    for tag, rtag, ptag, cells in (("ds_ne9", "ds_reproj9", "ds_prologue9", 10_000_000),
+                                   ("ds_ne93", "ds_reproj93", "ds_prologue93", 100_000_000)):
+        if tag not in want and rtag not in want and ptag not in want:
             continue
         suv, sxyz = util.sample_points(src, cells)
+        if ptag in want:  # initial error + linear estimation, one pass (48 B per point)
+            ms = timed(lambda: util.initial_error_and_linear_estimation(
+                conversion._init_target("double_sphere", src), sxyz, suv))
+            emit(ptag, sxyz.shape[0], ms, 48)
         ds = conversion._init_target("double_sphere", src)
         ds.linear_estimation(sxyz, suv)
         if tag in want:
