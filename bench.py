@@ -485,16 +485,21 @@ def leg_config5(ctx, n_cells):
     ctx.sync()
     t_s = ctx.max_over_ranks(time.perf_counter() - t0)
     allreduce = D.rccl_allreduce() if ctx.dist else None
-    ctx.sync()
-    t0 = time.perf_counter()
-    met = conversion.convert(src, "double_sphere", xyz, uv, allreduce=allreduce)
-    ctx.sync()
-    t_c = ctx.max_over_ranks(time.perf_counter() - t0)
+    # one untimed conversion first (its multi-GB workspaces' first
+    # allocation), then the fastest of three, each the max over ranks
+    conversion.convert(src, "double_sphere", xyz, uv, allreduce=allreduce)
+    t_c, met = float("inf"), None
+    for _ in range(3):
+        ctx.sync()
+        t0 = time.perf_counter()
+        met = conversion.convert(src, "double_sphere", xyz, uv, allreduce=allreduce)
+        ctx.sync()
+        t_c = min(t_c, ctx.max_over_ranks(time.perf_counter() - t0))
     out = {"what": "KB->DS conversion: sharded sample_points + linear estimation + bounded LM "
                    "+ reprojection errors",
            "requested_cells": n_cells, "grid": [ncx, ncy], "correspondences_total": total,
            "correspondences_rank0": int(uv.shape[0]), "sample_points_ms": round(t_s * 1e3, 3),
-           "convert_ms": round(t_c * 1e3, 3),
+           "convert_ms": round(t_c * 1e3, 3), "convert_timing": "warm, best of 3",
            "optimization_ms_rank0": round(met.optimization_time_ms, 3),
            "lm_iterations": met.lm_iterations, "termination": met.lm_termination,
            "final_mean_px": met.final_reprojection_error.mean,

@@ -66,6 +66,7 @@ for step in "$@"; do
     TAG=${TAG} bash tools/pmc_round.sh > $O/${TAG}_pmc_round.log 2>&1
     check $? pmc
     python3 profiles/collect_pmc.py $O/pmc_${TAG} --workload kb_project_jacobian_f64_aos \
+      --kernel "k_project_al<acm::Tag<acm::KannalaBrandt>" \
       --points 10000000 --algorithmic-bytes 1690000000 \
       --out $O/${TAG}_pmc_kb_project_jacobian.json > $O/${TAG}_collect_pmc.log 2>&1
     check $? collect_pmc ;;

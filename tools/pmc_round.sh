@@ -5,7 +5,7 @@ set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
-BA=${BENCH_ARGS:-"--steps 5 --warmup 1 --no-cpu-baseline"}
+BA=${BENCH_ARGS:-"--steps 5 --warmup 1 --no-cpu-baseline --legs none"}
 timeout -k 10 120 rocprofv3 -L > gpurun_out/rocprof_counters_list.txt 2>&1
 echo "list rc=$?"
 i=0
