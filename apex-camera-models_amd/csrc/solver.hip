@@ -268,13 +268,15 @@ ACM_API int acm_linear_estimation(acm_camera* cam, size_t n, const double* point
     rc = acm_linear_system_qr(cam, n, points_3d, layout, points_2d, d_r, d_err, workspace, qr,
                               stream);
     if (rc) return rc;
-    double R[16];
-    int err = 0;
+    // R (S <= 15 doubles) and the flag (at double 16) in one copy
+    double R[17];
     hipStream_t s = (hipStream_t)stream;
-    if (hip_ok(hipMemcpyAsync(R, d_r, S * sizeof(double), hipMemcpyDeviceToHost, s)) ||
-        hip_ok(hipMemcpyAsync(&err, d_err, sizeof(int), hipMemcpyDeviceToHost, s)) ||
+    (void)S;
+    if (hip_ok(hipMemcpyAsync(R, d_r, 17 * sizeof(double), hipMemcpyDeviceToHost, s)) ||
         hip_ok(hipStreamSynchronize(s)))
         return sfail(ACM_ERR_HIP, "linear estimation: device copy failed");
+    int err = 0;
+    std::memcpy(&err, &R[16], sizeof(int));
     return acm_linear_estimation_solve(cam, n, R, err);
 }
 
@@ -322,13 +324,15 @@ ACM_API int acm_linear_estimation_with_error(acm_camera* cam, size_t n, const do
     int rc = acm::linear_system_qr_error(cam, n, points_3d, layout, points_2d, d_r, d_err,
                                          initial_error, workspace, ws_err, stream);
     if (rc) return rc;
-    double R[16];
-    int err = 0;
+    // R (S <= 15 doubles) and the flag (at double 16) in one copy
+    double R[17];
     hipStream_t s = (hipStream_t)stream;
-    if (hip_ok(hipMemcpyAsync(R, d_r, S * sizeof(double), hipMemcpyDeviceToHost, s)) ||
-        hip_ok(hipMemcpyAsync(&err, d_err, sizeof(int), hipMemcpyDeviceToHost, s)) ||
+    (void)S;
+    if (hip_ok(hipMemcpyAsync(R, d_r, 17 * sizeof(double), hipMemcpyDeviceToHost, s)) ||
         hip_ok(hipStreamSynchronize(s)))
         return sfail(ACM_ERR_HIP, "linear estimation: device copy failed");
+    int err = 0;
+    std::memcpy(&err, &R[16], sizeof(int));
     return acm_linear_estimation_solve(cam, n, R, err);
 }
 

@@ -506,3 +506,69 @@ def test_initial_error_and_linear_estimation_errors():
     with pytest.raises(InvalidParams):
         util.initial_error_and_linear_estimation(m, torch.as_tensor(xyz[:3]),
                                                  torch.as_tensor(uv[:3]))
+
+
+def _capi_reprojection(L, cam, p3, p2, layout, n):
+    import ctypes
+    import torch
+    from apex_camera_models import _lib
+    wsb = L.acm_reprojection_error_workspace_size(n)
+    ws = torch.empty(((wsb + 7) // 8 + 1,), dtype=torch.float64, device="cuda")
+    res = torch.full((9,), -7.0, dtype=torch.float64, device="cuda")
+    _lib.check(L.acm_reprojection_error(ctypes.byref(cam), n, p3.data_ptr() if n else None,
+                                        layout, p2.data_ptr() if n else None, res.data_ptr(),
+                                        None, ws.data_ptr(), wsb,
+                                        torch.cuda.current_stream().cuda_stream))
+    return res.cpu().numpy()
+
+
+def test_reprojection_error_soa_layout_and_empty():
+    """acm_reprojection_error with the SoA point layout gives the AoS call's
+    result bit for bit (same per-point code, same partition); n = 0 gives
+    n_valid = 0 and a NaN median (the Python mirror then raises
+    ZeroProjectionPoints, error_metrics.rs:86)."""
+    import torch
+    from apex_camera_models import _lib
+    L = _lib.load()
+    uv, xyz, w, h = _sampled(KB, 200_000)
+    sp, _ = SAMPLES[KB]
+    m = _model(DS, sp[:4] + [0.5, 0.1], w, h)
+    cam = m.acm_camera()
+    n = xyz.shape[0]
+    p2 = torch.as_tensor(uv, device="cuda").contiguous()
+    aos = _capi_reprojection(L, cam, torch.as_tensor(xyz, device="cuda").contiguous(), p2,
+                             _lib.LAYOUT_AOS, n)
+    soa = _capi_reprojection(L, cam, torch.as_tensor(xyz.T.copy(), device="cuda"), p2,
+                             _lib.LAYOUT_SOA, n)
+    assert np.array_equal(aos, soa), (aos, soa)
+    assert aos[5] == n
+    empty = _capi_reprojection(L, cam, None, None, _lib.LAYOUT_AOS, 0)
+    assert empty[5] == 0 and np.isnan(empty[8])
+
+
+@pytest.mark.parametrize("target", [DS, KB, RADTAN])
+def test_linear_estimation_with_error_soa_layout(target):
+    """The fused opening with SoA points: the same initial error and the same
+    estimate as with AoS points, bit for bit."""
+    import ctypes
+    import torch
+    from apex_camera_models import _lib
+    L = _lib.load()
+    uv, xyz, w, h = _sampled(KB, 200_000)
+    sp, _ = SAMPLES[KB]
+    init = {KB: sp[:4] + [0.0] * 4, DS: sp[:4] + [0.5, 0.1], RADTAN: sp[:4] + [0.0] * 5}[target]
+    n = xyz.shape[0]
+    p2 = torch.as_tensor(uv, device="cuda").contiguous()
+    out = []
+    for layout, p3 in ((_lib.LAYOUT_AOS, torch.as_tensor(xyz, device="cuda").contiguous()),
+                       (_lib.LAYOUT_SOA, torch.as_tensor(xyz.T.copy(), device="cuda"))):
+        cam = _model(target, init, w, h).acm_camera()
+        wsb = L.acm_linear_estimation_with_error_workspace_size(target, n)
+        ws = torch.empty(((wsb + 7) // 8,), dtype=torch.float64, device="cuda")
+        res = torch.empty((9,), dtype=torch.float64, device="cuda")
+        _lib.check(L.acm_linear_estimation_with_error(
+            ctypes.byref(cam), n, p3.data_ptr(), layout, p2.data_ptr(), res.data_ptr(),
+            ws.data_ptr(), wsb, torch.cuda.current_stream().cuda_stream))
+        out.append((res.cpu().numpy(), list(cam.params)))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
