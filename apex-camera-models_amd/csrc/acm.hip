@@ -1953,7 +1953,11 @@ __global__ __launch_bounds__(kBlock) void k_seg_count(CamArg cam, Grid g, size_t
 // only those whose true offset differs and that keep something -- none at
 // all when nothing was dropped (total == cells).
 template <class TagT, int SPW, bool ILV, bool NT = false, bool FIX = false>
-__global__ __launch_bounds__(kBlock) void k_seg_write(CamArg cam, Grid g, size_t cells,
+// (r04) at least 6 waves per SIMD: the KB form (polynomial rays) drops from
+// 88 to 80 VGPRs without spills and writes 1e8 cells 3.5% faster (0.763 vs
+// 0.790 ms interleaved; 8 waves spill and gain 1.5%; the other models
+// already fit; profiles/r04t_seg_write_waves_ab.log)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_seg_write(CamArg cam, Grid g, size_t cells,
                                                       const uint32_t* __restrict__ seg_cnt,
                                                       const uint64_t* __restrict__ blk_off,
                                                       double* __restrict__ uv_out,
