@@ -105,6 +105,7 @@ EXPORTED_SYMBOLS = (
     "acm_reprojection_stats_workspace_size",
     "acm_reprojection_stats",
     "acm_reprojection_stats_merge",
+    "acm_project_unproject",
     "acm_reprojection_error_workspace_size",
     "acm_reprojection_error",
     "acm_linear_estimation_with_error_workspace_size",
@@ -203,6 +204,8 @@ def load():
     L.acm_error_stats.restype = i
     L.acm_reprojection_stats.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp, sz, vp]
     L.acm_reprojection_stats.restype = i
+    L.acm_project_unproject.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp, vp]
+    L.acm_project_unproject.restype = i
     L.acm_reprojection_error_workspace_size.argtypes = [sz]
     L.acm_reprojection_error_workspace_size.restype = sz
     L.acm_reprojection_error.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp, sz, vp]

@@ -644,6 +644,77 @@ __global__ __launch_bounds__(kBlock) void k_unproject(CamArg cam, size_t n,
     }
 }
 
+// Project -> unproject round trip in one pass (r04; BASELINE config 4, the
+// reference's per-point loop of tests/projection_accuracy.rs over mod.rs:256
+// and :271): each lane projects its points, stores the pixels and statuses
+// exactly as k_project does (NaN pixels for failed projections), then
+// unprojects those same pixel values from registers and stores rays and
+// statuses exactly as k_unproject does -- the bits of acm_project followed by
+// acm_unproject, without reading the 16 B per point of pixels back.
+template <class TagT, int LAYOUT, bool NT, int PPT, bool STG>
+__global__ __launch_bounds__(kBlock) void k_round_trip(CamArg cam, size_t n,
+                                                       const double* __restrict__ pts,
+                                                       double* __restrict__ uv,
+                                                       uint8_t* __restrict__ pstatus,
+                                                       double* __restrict__ rays,
+                                                       uint8_t* __restrict__ rstatus) {
+    using M = typename TagT::template type<double>;
+    const size_t i0 = (size_t)blockIdx.x * (kBlock * PPT) + threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const Cam<double> c = make_cam<double>(cam);
+    __shared__ double s_ray[STG ? kBlock / 64 : 1][STG ? 64 * 3 : 1];
+    double px[PPT], py[PPT], pz[PPT];
+#pragma unroll
+    for (int r = 0; r < PPT; ++r) {
+        const size_t i = i0 + (size_t)r * kBlock;
+        px[r] = py[r] = 0.0;
+        pz[r] = 1.0;
+        if (i < n) load_point<LAYOUT>(pts, n, i, px[r], py[r], pz[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < PPT; ++r) {
+        const size_t i = i0 + (size_t)r * kBlock;
+        const size_t wfirst = i - (size_t)lane;
+        if (wfirst >= n) break;  // wave-uniform
+        double X = 0.0, Y = 0.0, Z = 0.0;
+        uint8_t st = ST_OK;
+        if (i < n) {
+            double u, v;
+            const uint8_t sp = M::template project<false>(c, px[r], py[r], pz[r], u, v, nullptr,
+                                                          nullptr);
+            if (sp != ST_OK) u = v = __builtin_nan("");
+            st2<NT>(uv + 2 * i, u, v);
+            st1<NT>(pstatus + i, sp);
+            st = M::unproject(c, u, v, X, Y, Z);
+            if (st != ST_OK) X = Y = Z = __builtin_nan("");
+        }
+        if (LAYOUT == ACM_LAYOUT_AOS) {
+            if (STG && wfirst + 64 <= n) {  // whole wave in range
+                double* sr = s_ray[STG ? wid : 0];
+                sr[3 * lane] = X;
+                sr[3 * lane + 1] = Y;
+                sr[3 * lane + 2] = Z;
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                double* dst = rays + 3 * wfirst;
+                st2<NT>(dst + 2 * lane, sr[2 * lane], sr[2 * lane + 1]);
+                if (lane < 32) st2<NT>(dst + 128 + 2 * lane, sr[128 + 2 * lane], sr[129 + 2 * lane]);
+                __builtin_amdgcn_wave_barrier();
+            } else if (i < n) {
+                st1d<NT>(rays + 3 * i, X);
+                st1d<NT>(rays + 3 * i + 1, Y);
+                st1d<NT>(rays + 3 * i + 2, Z);
+            }
+        } else if (i < n) {
+            st1d<NT>(rays + i, X);
+            st1d<NT>(rays + n + i, Y);
+            st1d<NT>(rays + 2 * n + i, Z);
+        }
+        if (i < n) st1<NT>(rstatus + i, st);
+    }
+}
+
 // LDS-staged AoS ray stores by default for the models whose unprojection is
 // memory-bound (Pinhole, DS, UCM, EUCM, FOV: 6.0-6.4 -> 6.4-7.2 TB/s at 10M
 // pixels); the VALU-bound ones (KB, RadTan) lose 4-6% to the extra LDS and
@@ -3981,6 +4052,46 @@ ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_
         if (layout == ACM_LAYOUT_AOS) go(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else go(std::integral_constant<int, ACM_LAYOUT_SOA>{});
         return check_launch("acm_unproject");
+    });
+}
+
+ACM_API int acm_project_unproject(const acm_camera* cam, size_t n, const double* points_3d,
+                                  int layout, double* points_2d, uint8_t* status, double* rays,
+                                  uint8_t* ray_status, void* stream) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if (layout & (ACM_EXACT_MATH | ACM_REFERENCE_NEWTON)) {  // the two calls, in order
+        rc = acm_project(cam, n, points_3d, layout & ~ACM_REFERENCE_NEWTON, points_2d, status,
+                         nullptr, stream);
+        if (rc) return rc;
+        return acm_unproject(cam, n, points_2d, rays, layout & ~ACM_EXACT_MATH, ray_status,
+                             stream);
+    }
+    if ((rc = check_layout(layout))) return rc;
+    if (n == 0) return ACM_SUCCESS;
+    if (!points_3d || !points_2d || !status || !rays || !ray_status)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    hipStream_t s = (hipStream_t)stream;
+    return dispatch_model(cam->model, [&](auto tag) -> int {
+        using TagT = decltype(tag);
+        constexpr int K = 2;  // points per lane, as the unprojection
+        const bool nt = n * 42 > kNtThresholdBytes;
+        const bool stg = UnprojectStaged<TagT>::on && (reinterpret_cast<uintptr_t>(rays) & 15u) == 0;
+        const dim3 gk((unsigned)((n + (size_t)kBlock * K - 1) / ((size_t)kBlock * K))), b(kBlock);
+        auto go = [&](auto lay_c, auto stg_c) {
+            constexpr int L = decltype(lay_c)::value;
+            constexpr bool ST = decltype(stg_c)::value && L == ACM_LAYOUT_AOS;
+            auto kern = nt ? k_round_trip<TagT, L, true, K, ST> : k_round_trip<TagT, L, false, K, ST>;
+            hipLaunchKernelGGL(kern, gk, b, 0, s, prep(*cam, false), n, points_3d, points_2d,
+                               status, rays, ray_status);
+        };
+        if (layout == ACM_LAYOUT_AOS) {
+            if (stg) go(std::integral_constant<int, ACM_LAYOUT_AOS>{}, std::true_type{});
+            else go(std::integral_constant<int, ACM_LAYOUT_AOS>{}, std::false_type{});
+        } else {
+            go(std::integral_constant<int, ACM_LAYOUT_SOA>{}, std::false_type{});
+        }
+        return check_launch("acm_project_unproject");
     });
 }
 

@@ -349,10 +349,13 @@ def leg_config4(ctx, n_total, reps):
     `n_total` points in total (strong scaling: contiguous shards of one global
     batch), then ONE all-reduce of every model's (sum of squared round-trip
     errors, round-trip-ok count) -- the residual all-reduce of the config.
-    A step = the six round trips (12 launches, uv intermediate in HBM); the
-    error reduction runs after the timed steps, the all-reduce is timed on its
-    own.  The reference loop this batches: project then unproject per point
-    for every model (tests/projection_accuracy.rs, mod.rs:256/271)."""
+    A step = the six round trips, one acm_project_unproject launch per model
+    (r04: the pixels are written as by acm_project but unprojected from
+    registers instead of being read back; the 12-launch form of acm_project +
+    acm_unproject is timed beside it as `ms_per_step_two_calls`); the error
+    reduction runs after the timed steps, the all-reduce is timed on its own.
+    The reference loop this batches: project then unproject per point for
+    every model (tests/projection_accuracy.rs, mod.rs:256/271)."""
     import torch
     from apex_camera_models import _lib, samples
     from apex_camera_models.camera import MODEL_CLASSES, Resolution
@@ -379,6 +382,12 @@ def leg_config4(ctx, n_total, reps):
 
     def one(k):
         cam, (st, ray, st2) = cams[k], outs[k]
+        _lib.check(L.acm_project_unproject(ctypes.byref(cam), n, pts.data_ptr(), 0,
+                                           uv.data_ptr(), st.data_ptr(), ray.data_ptr(),
+                                           st2.data_ptr(), sh))
+
+    def one_two_calls(k):
+        cam, (st, ray, st2) = cams[k], outs[k]
         rc = L.acm_project(ctypes.byref(cam), n, pts.data_ptr(), 0, uv.data_ptr(), st.data_ptr(),
                            None, sh)
         rc = rc or L.acm_unproject(ctypes.byref(cam), n, uv.data_ptr(), ray.data_ptr(), 0,
@@ -386,9 +395,9 @@ def leg_config4(ctx, n_total, reps):
         if rc:
             _lib.check(rc)
 
-    def step():
+    def step(f=one):
         for k in range(len(cams)):
-            one(k)
+            f(k)
 
     step()
     ctx.sync()
@@ -400,6 +409,14 @@ def leg_config4(ctx, n_total, reps):
             one(k)
         ctx.sync()
         per_model.append(ctx.max_over_ranks((time.perf_counter() - t0) / reps * 1e3))
+    step(one_two_calls)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step(one_two_calls)
+    ctx.sync()
+    ms_two = ctx.max_over_ranks((time.perf_counter() - t0) / reps * 1e3)
+    step()
     ctx.sync()
     t0 = time.perf_counter()
     for _ in range(reps):
@@ -442,7 +459,7 @@ def leg_config4(ctx, n_total, reps):
     return {"what": "6 models x project->unproject round trip (strong: one global batch "
                     "sharded over the ranks) + all-reduce of (sum err^2, n_ok) per model",
             "points_total": n_total, "points_per_rank": n, "steps": reps,
-            "ms_per_step": round(ms, 4),
+            "ms_per_step": round(ms, 4), "ms_per_step_two_calls": round(ms_two, 4),
             "value": round(len(cams) * n_total / ms / 1e3, 1),
             "unit": "Mround-trips/s (all 6 models, whole job)",
             "scaling": "strong", "allreduce_us": None if coll_us is None else round(coll_us, 2),

@@ -174,6 +174,19 @@ ACM_API int acm_unproject(const acm_camera *cam, size_t n,
 /* Factor linearisation: residual r = project(p_i) - obs_i (2N) and the
  * 2N x P Jacobian (nullable) of *CameraParamsFactor
  * (camera_converter.rs:378 & co).  status nullable. */
+/* Project -> unproject round trip (BASELINE config 4; the reference's
+ * per-point loop of tests/projection_accuracy.rs over mod.rs:256 and :271)
+ * in one pass: writes exactly what acm_project (no Jacobian) followed by
+ * acm_unproject of its pixels writes -- points_2d (NaN where the projection
+ * failed), status, rays (NaN where the unprojection failed) and ray_status
+ * -- bit for bit, without reading the pixels back from memory.  layout as
+ * acm_project / acm_unproject; with ACM_EXACT_MATH or ACM_REFERENCE_NEWTON
+ * set it runs the two calls in order. (r04) */
+ACM_API int acm_project_unproject(const acm_camera *cam, size_t n,
+                                  const double *points_3d, int layout,
+                                  double *points_2d, uint8_t *status,
+                                  double *rays, uint8_t *ray_status,
+                                  void *stream);
 ACM_API int acm_residual_jacobian(const acm_camera *cam, size_t n,
                                   const double *points_3d, int layout,
                                   const double *points_2d_obs,

@@ -813,3 +813,43 @@ def test_newton_fast_random_cameras():
     assert failures == 0, failures
     for model in (1, 2):  # both paths of the per-camera switch were exercised
         assert min(covered[model]) >= 15, covered
+
+
+@pytest.mark.parametrize("layout", [0, 1])
+@pytest.mark.parametrize("n", [1, 257, 300_001])
+@pytest.mark.parametrize("model", range(7))
+def test_project_unproject_fused_matches_two_calls(model, n, layout):
+    """acm_project_unproject (BASELINE config 4's round trip in one pass)
+    writes exactly what acm_project followed by acm_unproject of its pixels
+    writes: pixels (NaN positions included), both statuses and the rays, bit
+    for bit, AoS and SoA, on the synthetic cloud with its edge points (z <= 0,
+    the origin, non-finite coordinates)."""
+    import ctypes
+    import torch
+    from apex_camera_models import _lib, samples
+    L = _lib.load()
+    params, (w, h) = samples.SAMPLES[model]
+    cam = _model_obj(model, params, w, h).acm_camera()
+    pts = samples.synthetic_points_device(n)
+    if layout == 1:
+        pts = pts.t().contiguous()
+    sh = torch.cuda.current_stream().cuda_stream
+
+    def bufs():
+        return (torch.full((n, 2), -1.0, dtype=torch.float64, device="cuda"),
+                torch.full((n,), 77, dtype=torch.uint8, device="cuda"),
+                torch.full((n, 3) if layout == 0 else (3, n), -1.0, dtype=torch.float64,
+                           device="cuda"),
+                torch.full((n,), 77, dtype=torch.uint8, device="cuda"))
+    a, b = bufs(), bufs()
+    _lib.check(L.acm_project(ctypes.byref(cam), n, pts.data_ptr(), layout, a[0].data_ptr(),
+                             a[1].data_ptr(), None, sh))
+    _lib.check(L.acm_unproject(ctypes.byref(cam), n, a[0].data_ptr(), a[2].data_ptr(), layout,
+                               a[3].data_ptr(), sh))
+    _lib.check(L.acm_project_unproject(ctypes.byref(cam), n, pts.data_ptr(), layout,
+                                       b[0].data_ptr(), b[1].data_ptr(), b[2].data_ptr(),
+                                       b[3].data_ptr(), sh))
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        xh, yh = x.cpu().numpy(), y.cpu().numpy()
+        assert xh.tobytes() == yh.tobytes() or np.array_equal(xh, yh, equal_nan=True)

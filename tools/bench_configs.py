@@ -284,6 +284,10 @@ def config4(n_per_model):
             L.acm_unproject(ctypes.byref(cam), n_per_model, uv.data_ptr(), ray.data_ptr(), 0,
                             st2.data_ptr(), sh)
 
+        ms_f = timed(lambda: L.acm_project_unproject(ctypes.byref(cam), n_per_model,
+                                                     pts.data_ptr(), 0, uv.data_ptr(),
+                                                     st.data_ptr(), ray.data_ptr(),
+                                                     st2.data_ptr(), sh))
         ms = timed(rt)
         ms_u = timed(lambda: L.acm_unproject(ctypes.byref(cam), n_per_model, uv.data_ptr(),
                                              ray.data_ptr(), 0, st2.data_ptr(), sh))
@@ -294,6 +298,8 @@ def config4(n_per_model):
               "round_trip_ms": round(ms, 4), "round_trip_Mpoints_per_s": round(
                   n_per_model / ms / 1e3, 1),
               "round_trip_GBps": round(82 * n_per_model / ms / 1e6, 1),
+              "fused_round_trip_ms": round(ms_f, 4),
+              "fused_round_trip_GBps": round(66 * n_per_model / ms_f / 1e6, 1),
               "unproject_ms": round(ms_u, 4),
               "unproject_GBps": round(41 * n_per_model / ms_u / 1e6, 1),
               "round_trip_ok": int(ok.sum()), "max_round_trip_err": float(err.max()),
