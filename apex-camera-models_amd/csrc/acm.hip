@@ -761,15 +761,44 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // Reduce K per-lane values across the workgroup into out[0..K) (LDS staged).
+// (r04) Wave reduce-scatter instead of K butterflies: KP - 1 + (6 - m)
+// shuffles per lane instead of 6 K (DS: 34 vs 150, KB: 63 vs 240) at the end
+// of every normal-equations workgroup; KB's call 0.084 -> 0.076 ms, DS at
+// 9.29M 0.068 -> 0.065 ms (profiles/r04w_ne_reduce_scatter_ab.log).  Another
+// summation order, fixed, so still bit-reproducible.
+constexpr int pow2_at_least(int k) { return k <= 1 ? 1 : 2 * pow2_at_least((k + 1) / 2); }
+constexpr int log2_exact(int k) { return k <= 1 ? 0 : 1 + log2_exact(k / 2); }
 template <int K>
 __device__ __forceinline__ void block_sum_store(const double (&acc)[K], double* __restrict__ out) {
     __shared__ double sm[kBlock / 64][K];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // wave reduce-scatter: with KP = 2^m >= K values per lane, each xor step
+    // hands half of a lane's remaining values to its partner and adds the
+    // half it keeps (KP - 1 shuffles in all instead of 6 K); lane l ends
+    // with value l >> (6 - m) summed over 2^m lanes, and 6 - m plain xor
+    // steps over the low lane bits finish the wave sum
+    constexpr int KP = pow2_at_least(K) < 64 ? pow2_at_least(K) : 64;
+    static_assert(K <= 64, "reduce-scatter over one wave");
+    constexpr int m = log2_exact(KP);
+    double v[KP];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const double s = wave_sum(acc[k]);
-        if (lane == 0) sm[wid][k] = s;
+    for (int k = 0; k < KP; ++k) v[k] = k < K ? acc[k] : 0.0;
+#pragma unroll
+    for (int st = 0; st < m; ++st) {
+        const int h = KP >> (st + 1), o = 32 >> st;
+        const bool up = (lane & o) != 0;
+#pragma unroll
+        for (int j = 0; j < h; ++j) {
+            const double send = up ? v[j] : v[j + h];
+            const double keep = up ? v[j + h] : v[j];
+            v[j] = keep + __shfl_xor(send, o, 64);
+        }
     }
+    double t = v[0];
+#pragma unroll
+    for (int o = (32 >> m); o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    const int idx = lane >> (6 - m);
+    if ((lane & ((1 << (6 - m)) - 1)) == 0 && idx < K) sm[wid][idx] = t;
     __syncthreads();
     for (int k = threadIdx.x; k < K; k += kBlock) {
         double s = 0.0;
