@@ -768,8 +768,12 @@ __device__ __forceinline__ double wave_sum(double v) {
 // summation order, fixed, so still bit-reproducible.
 constexpr int pow2_at_least(int k) { return k <= 1 ? 1 : 2 * pow2_at_least((k + 1) / 2); }
 constexpr int log2_exact(int k) { return k <= 1 ? 0 : 1 + log2_exact(k / 2); }
+// out[k * ostride], k < K (the normal equations' partials are column-major:
+// sum k of workgroup b at parts[k * nb + b], so k_ne_finish_cols reads each
+// column coalesced)
 template <int K>
-__device__ __forceinline__ void block_sum_store(const double (&acc)[K], double* __restrict__ out) {
+__device__ __forceinline__ void block_sum_store(const double (&acc)[K], double* __restrict__ out,
+                                                size_t ostride) {
     __shared__ double sm[kBlock / 64][K];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     // wave reduce-scatter: with KP = 2^m >= K values per lane, each xor step
@@ -804,7 +808,7 @@ __device__ __forceinline__ void block_sum_store(const double (&acc)[K], double* 
         double s = 0.0;
 #pragma unroll
         for (int w = 0; w < kBlock / 64; ++w) s += sm[w][k];
-        out[k] = s;
+        out[(size_t)k * ostride] = s;
     }
 }
 
@@ -1012,7 +1016,7 @@ struct NeAccum {
     }
 
     // workgroup sum of the lanes' sums -> out[0..K) in NE<P>'s layout
-    __device__ __forceinline__ void store(double* __restrict__ out) const {
+    __device__ __forceinline__ void store(double* __restrict__ out, size_t ostride) const {
         if constexpr (kKB) {  // expand the 37 KB sums into the NE<8> layout
             static_assert(K == 40, "NE<8>");
             double full[K];
@@ -1039,9 +1043,9 @@ struct NeAccum {
             full[L::G + 3] = acc[30];
             full[K - 2] = acc[35];
             full[K - 1] = acc[36];
-            block_sum_store<K>(full, out);
+            block_sum_store<K>(full, out, ostride);
         } else {
-            block_sum_store<K>(acc, out);
+            block_sum_store<K>(acc, out, ostride);
         }
     }
 };
@@ -1171,7 +1175,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             }
         }
     }
-    sums.store(parts + (size_t)blockIdx.x * K);
+    sums.store(parts + blockIdx.x, gridDim.x);
 }
 
 // Epilogue of k_normal_eq: sum the per-workgroup partials (nb x K,
@@ -1228,7 +1232,7 @@ __global__ __launch_bounds__(kBlock) void k_ne_finish_cols(const double* __restr
     __shared__ double s_sum;
     if (k < K) {
         double a = 0.0;
-        for (int b = threadIdx.x; b < nb; b += kBlock) a += parts[(size_t)b * K + k];
+        for (int b = threadIdx.x; b < nb; b += kBlock) a += parts[(size_t)k * nb + b];
         a = wave_sum(a);
         if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = a;
         __syncthreads();
