@@ -1220,11 +1220,15 @@ __device__ __forceinline__ int ne_out_src(int t) {
 }
 
 // SYS (the LM's host-polled path): each workgroup's results are made
-// visible at system scope before it ends, so the k_ne_publish that follows
-// in the stream can release the flag after all of them.
+// visible at system scope before it ends; then the workgroups take a ticket
+// and the last one releases the host's completion word (flag = seq) and
+// re-arms the ticket (ticket == nullptr: a k_ne_publish follows instead).
 template <int P, bool SYS>
 __global__ __launch_bounds__(kBlock) void k_ne_finish_cols(const double* __restrict__ parts, int nb,
-                                                           double* __restrict__ out) {
+                                                           double* __restrict__ out,
+                                                           unsigned int* __restrict__ ticket,
+                                                           unsigned long long* __restrict__ flag,
+                                                           unsigned long long seq) {
     using L = NE<P>;
     constexpr int K = L::K, NOUT = P * P + P + 2;
     const int k = blockIdx.x;
@@ -1249,7 +1253,20 @@ __global__ __launch_bounds__(kBlock) void k_ne_finish_cols(const double* __restr
         for (int t = threadIdx.x; t < NOUT; t += kBlock)
             if (ne_out_src<P>(t) < 0) out[t] = 0.0;
     }
-    if (SYS) __threadfence_system();
+    if (SYS) {
+        __threadfence_system();
+        if (ticket) {  // the last workgroup releases the host's completion word
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                if (t == gridDim.x - 1) {
+                    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
+        }
+    }
 }
 
 // The LM's host-polled path after k_ne_finish_cols: every result is out
@@ -4196,7 +4213,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
                           const double* points_2d_obs, int invalid_policy, double* result,
                           void* workspace, size_t workspace_bytes, void* stream,
                           unsigned long long* flag, unsigned long long seq,
-                          const double* dparams, const int* ddone) {
+                          const double* dparams, const int* ddone, unsigned int* ticket) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -4245,13 +4262,18 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
         };
         if (layout == ACM_LAYOUT_AOS) by_waves(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else by_waves(std::integral_constant<int, ACM_LAYOUT_SOA>{});
+        // (r04) with a ticket the finish kernel's last workgroup releases
+        // the completion word itself: one launch fewer per LM evaluation
+        // (host loop 1.275 -> 1.252 ms at config 3, three interleaved runs,
+        // profiles/r04t2_lm_ticket_ab.log)
+        unsigned int* tk = ticket;
         if (flag) {
             hipLaunchKernelGGL((k_ne_finish_cols<P, true>), dim3(NE<P>::K + 1), dim3(kBlock), 0, s,
-                               parts, nb, result);
-            hipLaunchKernelGGL(k_ne_publish, dim3(1), dim3(1), 0, s, flag, seq);
+                               parts, nb, result, tk, flag, seq);
+            if (!tk) hipLaunchKernelGGL(k_ne_publish, dim3(1), dim3(1), 0, s, flag, seq);
         } else {
             hipLaunchKernelGGL((k_ne_finish_cols<P, false>), dim3(NE<P>::K + 1), dim3(kBlock), 0, s,
-                               parts, nb, result);
+                               parts, nb, result, nullptr, nullptr, 0ull);
         }
         return check_launch("acm_normal_equations");
     });
@@ -4283,7 +4305,7 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
                                  void* stream) {
     return acm::normal_equations_impl(cam, n, points_3d, layout, points_2d_obs, invalid_policy,
                                       result, workspace, workspace_bytes, stream, nullptr, 0,
-                                      nullptr, nullptr);
+                                      nullptr, nullptr, nullptr);
 }
 
 ACM_API size_t acm_reprojection_stats_workspace_size(size_t n) {

@@ -29,7 +29,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
                           const double* points_2d_obs, int invalid_policy, double* result,
                           void* workspace, size_t workspace_bytes, void* stream,
                           unsigned long long* flag, unsigned long long seq,
-                          const double* dparams, const int* ddone);
+                          const double* dparams, const int* ddone, unsigned int* ticket);
 int lm_device();                                   // acm.hip, ACM_TUNE_LM_DEVICE
 int lm_step_launch(int P, lm::State* st, const acm_lm_config& cfg, const double* res,
                    double* dparams, int* ddone, unsigned long long* hflag,
@@ -408,9 +408,17 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
         else
             (void)hipGetLastError();
     }
+    // the finish kernel's ticket (mode 2): one of d_res's spare words, zeroed
+    // here and re-armed by the last workgroup of every evaluation
+    unsigned int* ticket = nullptr;
     if (host_mode && pinned) {
         res_out = pinned;
-        if (host_mode == 2) flag = reinterpret_cast<unsigned long long*>(pinned + 127);
+        if (host_mode == 2) {
+            flag = reinterpret_cast<unsigned long long*>(pinned + 127);
+            ticket = reinterpret_cast<unsigned int*>(d_res + R);
+            if (hip_ok(hipMemsetAsync(ticket, 0, sizeof(unsigned int), s)))
+                return sfail(ACM_ERR_HIP, "LM: ticket reset failed");
+        }
     }
     // evaluate [JtJ | Jtr | 0.5 r.r | n_valid] at parameter vector x (the
     // host loop)
@@ -420,7 +428,7 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
         const unsigned long long want = flag ? ++seq : 0;
         int rc = acm::normal_equations_impl(&c, n, points_3d, layout, points_2d,
                                             cfg->invalid_policy, res_out, workspace, ne_ws, stream,
-                                            flag, want, nullptr, nullptr);
+                                            flag, want, nullptr, nullptr, ticket);
         if (rc) return rc;
         if (allreduce) {
             rc = allreduce(allreduce_ctx, d_res, (size_t)R, stream);
@@ -483,7 +491,7 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
         auto enqueue = [&]() -> int {
             int rc = acm::normal_equations_impl(cam, n, points_3d, layout, points_2d,
                                                 cfg->invalid_policy, d_res, workspace, ne_ws,
-                                                stream, nullptr, 0, d_par, d_done);
+                                                stream, nullptr, 0, d_par, d_done, nullptr);
             if (rc) return rc;
             return acm::lm_step_launch(P, d_st, *cfg, d_res, d_par, d_done, hflag, ++queued,
                                        stream);
