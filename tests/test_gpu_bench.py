@@ -40,6 +40,8 @@ def test_bench_single_gpu_line():
     assert d["collective"]["global_n_valid"] > 0.99 * 300000
     assert "traffic_source" in d["roofline"]
     assert d["config4"]["points_total"] == 50_000_000 and d["config4"]["value"] > 0
+    # the one-pass round trip and the twelve-launch form it replaces, both timed
+    assert 0 < d["config4"]["ms_per_step"] and 0 < d["config4"]["ms_per_step_two_calls"]
     assert d["config5"]["correspondences_total"] == 92_935_075
     assert d["config5"]["final_mean_px"] < 0.01
 
