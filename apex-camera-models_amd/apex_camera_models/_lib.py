@@ -73,7 +73,7 @@ TUNE_NEWTON_FAST = 12  # removed in round 3: acm_set_tuning rejects it (use REFE
 TUNE_UNPROJECT_PPT = 13
 TUNE_SAMPLE_CERT = 14
 TUNE_SAMPLE_WRITE = 15
-TUNE_LM_DEVICE = 16  # r04: LM state machine on the device (k_lm_step)
+TUNE_LM_DEVICE = 16  # removed in r05 (acm_set_tuning: ACM_ERR_NOT_SUPPORTED)
 ERR_NOT_SUPPORTED = -6
 ERR_NUMERICAL = -7
 LM_TERMINATION = {0: "MaxIterations", 1: "CostTolerance", 2: "ParameterTolerance",

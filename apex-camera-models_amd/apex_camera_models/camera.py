@@ -257,6 +257,31 @@ class CameraModel:
                                               _stream_handle()))
         return rays, st
 
+    def project_unproject_batch(self, points_3d, layout: str = "aos"):
+        """Project then unproject every point in one pass (acm_project_unproject;
+        the per-point loop of tests/projection_accuracy.rs:49-73 over
+        mod.rs:256 and :271, BASELINE config 4).  Returns (uv, status, rays,
+        ray_status): the pixels as project_batch writes them (NaN for failed
+        projections) and the unprojection of those same pixels."""
+        lay = _lib.LAYOUT_SOA if layout == "soa" else _lib.LAYOUT_AOS
+        if lay == _lib.LAYOUT_AOS:
+            pts = _as_device_f64(points_3d, 3)
+        else:
+            pts = torch.as_tensor(points_3d, dtype=torch.float64).to("cuda").reshape(
+                3, -1).contiguous()
+        n = pts.shape[0] if lay == _lib.LAYOUT_AOS else pts.shape[1]
+        uv = torch.empty((n, 2), dtype=torch.float64, device=pts.device)
+        st = torch.empty((n,), dtype=torch.uint8, device=pts.device)
+        rays = torch.empty((n, 3) if lay == _lib.LAYOUT_AOS else (3, n), dtype=torch.float64,
+                           device=pts.device)
+        st2 = torch.empty((n,), dtype=torch.uint8, device=pts.device)
+        cam = self.acm_camera()
+        _lib.check(_lib.load().acm_project_unproject(ctypes.byref(cam), n, pts.data_ptr(), lay,
+                                                      uv.data_ptr(), st.data_ptr(),
+                                                      rays.data_ptr(), st2.data_ptr(),
+                                                      _stream_handle()))
+        return uv, st, rays, st2
+
     # --- linear_estimation (GPU TSQR + host k x k SVD solve) ---------------
     def linear_estimation(self, points_3d, points_2d) -> None:
         """`XModel::linear_estimation(&Matrix3xX, &Matrix2xX)` (kannala_brandt.rs:164-272,

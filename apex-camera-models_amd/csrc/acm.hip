@@ -31,7 +31,6 @@
 
 #include "acm.h"
 #include "camera_models.hpp"
-#include "lm_core.hpp"
 
 namespace acm {
 
@@ -326,12 +325,6 @@ int lm_host_result() {
     const int v = g_lm_host_result.load(std::memory_order_relaxed);
     return v < 0 ? 2 : v;
 }
-// acm_lm_optimize without an all-reduce callback runs the LM state machine on
-// the device (k_lm_step behind each evaluation, r04): -1 = auto (= off until
-// measured faster), 0 = the host loop, 1 = on.  Bit-identical iterates
-// (lm_core.hpp).
-static std::atomic<int> g_lm_device{-1};
-int lm_device() { return g_lm_device.load(std::memory_order_relaxed) > 0; }
 // Outputs above this many bytes are stored non-temporally.  Measured at 10M
 // points (profiles/r01_diag_ntl.log): project without J (170 MB out) 0.056 ms
 // nt vs 0.072 plain; a consumer that re-reads a smaller output soon after
@@ -1058,21 +1051,10 @@ template <class TagT, int LAYOUT, int WAVES, int U, bool NTL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq(acm_camera cam, size_t n,
                                                       const double* __restrict__ pts,
                                                       const double* __restrict__ obs, int policy,
-                                                      double* __restrict__ parts,
-                                                      const double* __restrict__ dparams,
-                                                      const int* __restrict__ ddone) {
+                                                      double* __restrict__ parts) {
     using Acc = NeAccum<TagT>;
     constexpr int K = Acc::K;
-    // the device-resident LM (r04): an evaluation queued after the run ended
-    // does nothing, and the parameters come from the previous k_lm_step (the
-    // projections read no host-derived constant of them; FOV's tan(w / 2)
-    // is one, so FOV keeps the host loop)
-    if (ddone && *ddone) return;
-    Cam<double> c = make_cam<double>(cam);
-    if (dparams) {
-#pragma unroll
-        for (int p = 0; p < Acc::P; ++p) c.p[p] = dparams[p];
-    }
+    const Cam<double> c = make_cam<double>(cam);
     Acc sums;
     sums.init();
     const double sent2 = policy == ACM_INVALID_SENTINEL ? 2e12 : 0.0;
@@ -1271,57 +1253,6 @@ __global__ __launch_bounds__(kBlock) void k_ne_finish_cols(const double* __restr
 
 // The LM's host-polled path after k_ne_finish_cols: every result is out
 // (stream order), publish `seq` with a system-scope release.
-// One step of the device-resident LM (r04; lm_core.hpp): one thread takes
-// the evaluation k_ne_finish_cols just wrote (res), advances the state
-// machine to the next evaluation -- writing its parameters where the next
-// queued k_normal_eq reads them -- or ends the run (*ddone = 1), then
-// publishes the number of completed steps (and the end) in host-mapped
-// memory for the host's enqueue loop.  A step queued after the end returns
-// at once, so the host may run a few evaluations ahead.
-// The state is copied into registers (P is a template constant: every loop
-// of lm_core.hpp unrolls) and written back; the host reads only the two
-// flag words, so they need no release fence.
-template <int P>
-__global__ __launch_bounds__(64) void k_lm_step(lm::State* __restrict__ st, acm_lm_config cfg,
-                          const double* __restrict__ res, double* __restrict__ dparams,
-                          int* __restrict__ ddone, unsigned long long* __restrict__ hflag,
-                          unsigned long long seq) {
-    if (threadIdx.x != 0 || *ddone) return;
-    // The one working lane reads the state and the results through an
-    // opaque (divergent) lane offset, 0 here: uniform loads would put the
-    // ~140 doubles in SGPRs, where FP64 cannot be computed on, and spill
-    // (hundreds of SGPR spills to scratch).  Element-wise copies with
-    // constant indices then split the state into VGPRs.
-    unsigned off = threadIdx.x;
-    asm volatile("" : "+v"(off));
-    st += off;
-    res += off;
-    lm::State s;
-    auto io = [&](lm::State& d, const lm::State& a) {
-        d.P = a.P; d.it = a.it; d.evals = a.evals; d.term = a.term; d.phase = a.phase;
-        d.F = a.F; d.nv = a.nv; d.mu = a.mu; d.nu = a.nu; d.dmax = a.dmax;
-        d.initial_cost = a.initial_cost;
-#pragma unroll
-        for (int i = 0; i < P; ++i) {
-            d.x[i] = a.x[i]; d.xn[i] = a.xn[i]; d.h[i] = a.h[i]; d.g[i] = a.g[i];
-        }
-#pragma unroll
-        for (int i = 0; i < P * P; ++i) d.A[i] = a.A[i];
-    };
-    io(s, *st);
-    const int r = lm::consume(s, cfg, res, P);
-    io(*st, s);
-    if (r == lm::DONE) {
-        *ddone = 1;
-    } else {
-#pragma unroll
-        for (int p = 0; p < P; ++p) dparams[p] = s.xn[p];
-    }
-    __hip_atomic_store(hflag + 1, (unsigned long long)(r == lm::DONE), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(hflag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 __global__ void k_ne_publish(unsigned long long* __restrict__ flag, unsigned long long seq) {
     __threadfence_system();
     __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -4207,13 +4138,11 @@ ACM_API size_t acm_normal_equations_workspace_size(int model, size_t n) {
 extern "C++" {
 namespace acm {
 // flag / seq: see k_ne_finish_cols / k_ne_publish (the LM's polled path in solver.hip)
-// dparams / ddone (the device-resident LM): parameters read by the kernel
-// from device memory, and the run's end flag (see k_normal_eq, k_lm_step).
 int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                           const double* points_2d_obs, int invalid_policy, double* result,
                           void* workspace, size_t workspace_bytes, void* stream,
                           unsigned long long* flag, unsigned long long seq,
-                          const double* dparams, const int* ddone, unsigned int* ticket) {
+                          unsigned int* ticket) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -4251,7 +4180,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
-                               points_2d_obs, invalid_policy, parts, dparams, ddone);
+                               points_2d_obs, invalid_policy, parts);
         };
         auto by_waves = [&](auto lay_c) {
             switch (wv) {
@@ -4279,23 +4208,6 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
     });
 }
 
-int lm_step_launch(int P, lm::State* st, const acm_lm_config& cfg, const double* res,
-                   double* dparams, int* ddone, unsigned long long* hflag,
-                   unsigned long long seq, void* stream) {
-    hipStream_t s = (hipStream_t)stream;
-    auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, s, st, cfg, res, dparams, ddone, hflag, seq);
-    };
-    switch (P) {
-    case 4: go(k_lm_step<4>); break;
-    case 5: go(k_lm_step<5>); break;
-    case 6: go(k_lm_step<6>); break;
-    case 8: go(k_lm_step<8>); break;
-    case 9: go(k_lm_step<9>); break;
-    default: return fail(ACM_ERR_NOT_SUPPORTED, "LM step: unsupported parameter count");
-    }
-    return check_launch("acm_lm_optimize (k_lm_step)");
-}
 }  // namespace acm
 }  // extern "C++"
 
@@ -4305,7 +4217,7 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
                                  void* stream) {
     return acm::normal_equations_impl(cam, n, points_3d, layout, points_2d_obs, invalid_policy,
                                       result, workspace, workspace_bytes, stream, nullptr, 0,
-                                      nullptr, nullptr, nullptr);
+                                      nullptr);
 }
 
 ACM_API size_t acm_reprojection_stats_workspace_size(size_t n) {
@@ -5067,12 +4979,14 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_SAMPLE_CERT, &g_sample_cert, -1, 0, "value must be -1 (auto) or 0"},
         {ACM_TUNE_SAMPLE_WRITE, &g_sample_write, -1, 5, "value must be -1..5"},
         {ACM_TUNE_UNPROJECT_PPT, &g_unproject_ppt, -1, 3, "value must be -1..3"},
-        {ACM_TUNE_LM_DEVICE, &g_lm_device, -1, 1, "value must be -1..1"},
     };
     if (key == ACM_TUNE_NEWTON_FAST)  // removed (r03): numerics are chosen per call
         return fail(ACM_ERR_NOT_SUPPORTED,
                     "ACM_TUNE_NEWTON_FAST was removed: OR ACM_REFERENCE_NEWTON into the call's "
                     "layout / flags instead (acm_unproject, acm_sample_points_ex)");
+    if (key == ACM_TUNE_LM_DEVICE)  // removed (r05): slower than the host loop
+        return fail(ACM_ERR_NOT_SUPPORTED,
+                    "ACM_TUNE_LM_DEVICE was removed: acm_lm_optimize runs the host loop");
     for (const Knob& k : knobs) {
         if (k.key != key) continue;
         bool ok = value >= k.lo && value <= k.hi;

@@ -1,12 +1,10 @@
 // lm_core.hpp -- the bounded Levenberg-Marquardt state machine of
-// acm_lm_optimize (solver.hip) as __host__ __device__ code.  Two drivers run
-// it: the host loop (used with a cross-rank all-reduce callback, and as
-// ACM_TUNE_LM_DEVICE = 0) and the device-resident loop (r04: k_lm_step in
-// acm.hip, one thread, queued behind each evaluation's normal equations so
-// the host never sits between two evaluations).  Both execute the same IEEE
-// operations in the same order (no FMA contraction: -ffp-contract=off on
-// both sides, correctly rounded sqrt and division on both), so they take
-// the same iterates bit for bit.
+// acm_lm_optimize (solver.hip), host code: start() clamps the start point,
+// then the driver alternates one normal-equations evaluation on the GPU
+// (k_normal_eq + k_ne_finish_cols) with consume(), which advances the state
+// to the next parameter vector to evaluate or ends the run.  (r04 also ran
+// this state machine on the device, behind each evaluation; it measured
+// slower than the host loop and was removed in r05.)
 //
 // Reference: bin/camera_converter.rs:381-420 (apex-solver LM with bounds,
 // max_iterations = 100, cost_tolerance = 1e-6, parameter_tolerance = 1e-8,
@@ -19,10 +17,6 @@
 #include <math.h>
 
 #include "acm.h"
-
-#ifndef ACM_LM_HD
-#define ACM_LM_HD __host__ __device__
-#endif
 
 namespace acm {
 namespace lm {
@@ -38,24 +32,11 @@ struct State {
     double F, nv, mu, nu, dmax, initial_cost;
 };
 
-// Every function is force-inlined and takes P as its first argument: the
-// device step kernel (k_lm_step<P>) calls them with a compile-time P, so the
-// loops unroll and the state lives in registers (with a run-time P the
-// arrays' dynamic indexing went to scratch: ~30-50 us per step).
-#if defined(__HIP_DEVICE_COMPILE__)
-#define ACM_LM_UNROLL _Pragma("unroll")
-#else
-#define ACM_LM_UNROLL
-#endif
-
-ACM_LM_HD __forceinline__ bool cholesky_solve(int P, const double* A, const double* b, double* x) {
+inline bool cholesky_solve(int P, const double* A, const double* b, double* x) {
     double L[81];
-    ACM_LM_UNROLL
     for (int i = 0; i < P; ++i)
-        ACM_LM_UNROLL
         for (int j = 0; j <= i; ++j) {
             double s = A[i * P + j];
-            ACM_LM_UNROLL
             for (int q = 0; q < j; ++q) s -= L[i * P + q] * L[j * P + q];
             if (i == j) {
                 if (!(s > 0.0)) return false;
@@ -65,50 +46,41 @@ ACM_LM_HD __forceinline__ bool cholesky_solve(int P, const double* A, const doub
             }
         }
     double y[9];
-    ACM_LM_UNROLL
     for (int i = 0; i < P; ++i) {
         double s = b[i];
-        ACM_LM_UNROLL
         for (int q = 0; q < i; ++q) s -= L[i * P + q] * y[q];
         y[i] = s / L[i * P + i];
     }
-    ACM_LM_UNROLL
     for (int i = P - 1; i >= 0; --i) {
         double s = y[i];
-        ACM_LM_UNROLL
         for (int q = i + 1; q < P; ++q) s -= L[q * P + i] * x[q];
         x[i] = s / L[i * P + i];
     }
     return true;
 }
 
-ACM_LM_HD __forceinline__ void clamp(const acm_lm_config& cfg, int P, double* x) {
+inline void clamp(const acm_lm_config& cfg, int P, double* x) {
     if (!cfg.has_bounds) return;
-    ACM_LM_UNROLL
     for (int i = 0; i < P; ++i) x[i] = fmin(fmax(x[i], cfg.lower[i]), cfg.upper[i]);
 }
 
-ACM_LM_HD __forceinline__ double ginf(int P, const double* g) {
+inline double ginf(int P, const double* g) {
     double m = 0.0;
-    ACM_LM_UNROLL
     for (int i = 0; i < P; ++i) m = fmax(m, fabs(g[i]));
     return m;
 }
 
 // The start point: the parameters, clamped; the first evaluation is at xn.
-ACM_LM_HD __forceinline__ void start(State& s, const acm_lm_config& cfg, int P, const double* params) {
+inline void start(State& s, const acm_lm_config& cfg, int P, const double* params) {
     s.P = P;
     s.it = 0;
     s.evals = 0;
     s.term = ACM_LM_MAX_ITERATIONS;
     s.phase = 0;
     s.pad = 0;
-    ACM_LM_UNROLL
     for (int i = 0; i < 9; ++i) s.x[i] = s.xn[i] = s.h[i] = 0.0;
-    ACM_LM_UNROLL
     for (int i = 0; i < P; ++i) s.x[i] = params[i];
     clamp(cfg, P, s.x);
-    ACM_LM_UNROLL
     for (int i = 0; i < P; ++i) s.xn[i] = s.x[i];
     s.F = s.nv = s.mu = s.nu = s.dmax = s.initial_cost = 0.0;
 }
@@ -116,14 +88,12 @@ ACM_LM_HD __forceinline__ void start(State& s, const acm_lm_config& cfg, int P, 
 // Iterate until the next evaluation is needed (NEED_EVAL, s.xn and s.h set)
 // or the run ends (DONE, s.term set).  Cholesky failures raise the damping
 // and retry without an evaluation, as does nothing else.
-ACM_LM_HD __forceinline__ int advance(State& s, const acm_lm_config& cfg, int P) {
+inline int advance(State& s, const acm_lm_config& cfg, int P) {
     while (s.term == ACM_LM_MAX_ITERATIONS && s.it < cfg.max_iterations) {
         ++s.it;
         // (JtJ + mu * diag(JtJ)) h = -g   (Marquardt scaling, floored)
         double Ad[81], mg[9], hstep[9];
-        ACM_LM_UNROLL
         for (int i = 0; i < P * P; ++i) Ad[i] = s.A[i];
-        ACM_LM_UNROLL
         for (int i = 0; i < P; ++i) {
             Ad[i * P + i] += s.mu * fmax(s.A[i * P + i], 1e-12 * fmax(s.dmax, 1.0));
             mg[i] = -s.g[i];
@@ -134,10 +104,8 @@ ACM_LM_HD __forceinline__ int advance(State& s, const acm_lm_config& cfg, int P)
             continue;
         }
         double xnorm = 0.0, hnorm = 0.0;
-        ACM_LM_UNROLL
         for (int i = 0; i < P; ++i) s.xn[i] = s.x[i] + hstep[i];
         clamp(cfg, P, s.xn);
-        ACM_LM_UNROLL
         for (int i = 0; i < P; ++i) {
             s.h[i] = s.xn[i] - s.x[i];
             hnorm += s.h[i] * s.h[i];
@@ -157,22 +125,19 @@ ACM_LM_HD __forceinline__ int advance(State& s, const acm_lm_config& cfg, int P)
 // Take the evaluation at s.xn -- res = [JtJ (P x P) | Jtr (P) | 0.5 r.r |
 // n_valid], acm_normal_equations' layout -- then advance.  P == s.P (a
 // compile-time constant in the device step kernel).
-ACM_LM_HD __forceinline__ int consume(State& s, const acm_lm_config& cfg, const double* res,
+inline int consume(State& s, const acm_lm_config& cfg, const double* res,
                                       int P) {
     ++s.evals;
     const double* An = res;
     const double* gn = res + P * P;
     const double Fn = res[P * P + P], nvn = res[P * P + P + 1];
     if (s.phase == 0) {
-        ACM_LM_UNROLL
         for (int i = 0; i < P * P; ++i) s.A[i] = An[i];
-        ACM_LM_UNROLL
         for (int i = 0; i < P; ++i) s.g[i] = gn[i];
         s.F = Fn;
         s.nv = nvn;
         s.initial_cost = Fn;
         s.dmax = 0.0;
-        ACM_LM_UNROLL
         for (int i = 0; i < P; ++i) s.dmax = fmax(s.dmax, s.A[i * P + i]);
         s.mu = cfg.initial_damping;
         s.nu = 2.0;
@@ -183,11 +148,9 @@ ACM_LM_HD __forceinline__ int consume(State& s, const acm_lm_config& cfg, const 
     }
     // predicted reduction L(0) - L(h) = -(g.h + 0.5 h.A.h)
     double gh = 0.0, hAh = 0.0;
-    ACM_LM_UNROLL
     for (int i = 0; i < P; ++i) {
         gh += s.g[i] * s.h[i];
         double t = 0.0;
-        ACM_LM_UNROLL
         for (int j = 0; j < P; ++j) t += s.A[i * P + j] * s.h[j];
         hAh += s.h[i] * t;
     }
@@ -196,11 +159,8 @@ ACM_LM_HD __forceinline__ int consume(State& s, const acm_lm_config& cfg, const 
     if (rho > 0.0) {
         const double dF = s.F - Fn;
         const double Fold = s.F;
-        ACM_LM_UNROLL
         for (int i = 0; i < P; ++i) s.x[i] = s.xn[i];
-        ACM_LM_UNROLL
         for (int i = 0; i < P * P; ++i) s.A[i] = An[i];
-        ACM_LM_UNROLL
         for (int i = 0; i < P; ++i) s.g[i] = gn[i];
         s.F = Fn;
         s.nv = nvn;

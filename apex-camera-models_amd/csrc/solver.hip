@@ -29,11 +29,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
                           const double* points_2d_obs, int invalid_policy, double* result,
                           void* workspace, size_t workspace_bytes, void* stream,
                           unsigned long long* flag, unsigned long long seq,
-                          const double* dparams, const int* ddone, unsigned int* ticket);
-int lm_device();                                   // acm.hip, ACM_TUNE_LM_DEVICE
-int lm_step_launch(int P, lm::State* st, const acm_lm_config& cfg, const double* res,
-                   double* dparams, int* ddone, unsigned long long* hflag,
-                   unsigned long long seq, void* stream);
+                          unsigned int* ticket);
 int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                            const double* points_2d, double* r_factor, int* error_flag,
                            double* result, void* ws_qr, void* ws_err, void* stream);
@@ -353,14 +349,11 @@ ACM_API void acm_lm_default_config(acm_lm_config* cfg) {
 }
 
 // LM workspace: the normal equations' partials | the results (R doubles + 8
-// spare) | the device-resident loop's state, parameters and end flag (r04).
-constexpr size_t kLmDevBytes = (sizeof(acm::lm::State) + 16 * sizeof(double) + 64 + 255) / 256 * 256;
-
+// spare, one of them the finish kernel's ticket).
 ACM_API size_t acm_lm_workspace_size(int model, size_t n) {
     const int P = acm_num_params(model);
     if (P < 0) return 0;
-    return acm_normal_equations_workspace_size(model, n) + (size_t)(P * P + P + 2 + 8) * 8 +
-           kLmDevBytes;
+    return acm_normal_equations_workspace_size(model, n) + (size_t)(P * P + P + 2 + 8) * 8;
 }
 
 ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, int layout,
@@ -398,7 +391,6 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
     const int host_mode = allreduce ? 0 : acm::lm_host_result();
     double* res_out = d_res;
     unsigned long long* flag = nullptr;
-    // (the device-resident loop publishes its step count in words 120-121)
     if (!allreduce && !pinned) {
         void* p = nullptr;
         if (hipHostMalloc(&p, 128 * sizeof(double),
@@ -428,7 +420,7 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
         const unsigned long long want = flag ? ++seq : 0;
         int rc = acm::normal_equations_impl(&c, n, points_3d, layout, points_2d,
                                             cfg->invalid_policy, res_out, workspace, ne_ws, stream,
-                                            flag, want, nullptr, nullptr, ticket);
+                                            flag, want, ticket);
         if (rc) return rc;
         if (allreduce) {
             rc = allreduce(allreduce_ctx, d_res, (size_t)R, stream);
@@ -463,73 +455,17 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
 
     acm::lm::State st;
     acm::lm::start(st, *cfg, P, cam->params);
-    // The device-resident loop (ACM_TUNE_LM_DEVICE, r04): each evaluation is
-    // k_normal_eq (parameters from device memory) -> k_ne_finish_cols ->
-    // k_lm_step, and the host keeps kAhead evaluations queued, watching the
-    // steps' count in host-mapped memory -- no host round trip between two
-    // evaluations.  Not with an all-reduce (the sums must pass through the
-    // host-side callback) nor for FOV (its projection reads tan(w / 2), a
-    // host-computed constant of the parameters).
-    const bool dev = acm::lm_device() && !allreduce && cam->model != ACM_FOV && pinned;
-    if (dev) {
-        char* base = (char*)workspace + need - kLmDevBytes;
-        acm::lm::State* d_st = reinterpret_cast<acm::lm::State*>(base);
-        double* d_par = reinterpret_cast<double*>(base + sizeof(acm::lm::State));
-        int* d_done = reinterpret_cast<int*>(d_par + 16);
-        unsigned long long* hflag = reinterpret_cast<unsigned long long*>(pinned + 120);
-        __atomic_store_n(hflag, 0ull, __ATOMIC_RELEASE);
-        __atomic_store_n(hflag + 1, 0ull, __ATOMIC_RELEASE);
-        const int zero = 0;
-        if (hip_ok(hipMemcpyAsync(d_st, &st, sizeof(st), hipMemcpyHostToDevice, s)) ||
-            hip_ok(hipMemcpyAsync(d_par, st.xn, 9 * sizeof(double), hipMemcpyHostToDevice, s)) ||
-            hip_ok(hipMemcpyAsync(d_done, &zero, sizeof(int), hipMemcpyHostToDevice, s)) ||
-            hip_ok(hipStreamSynchronize(s)))
-            return sfail(ACM_ERR_HIP, "LM: device state upload failed");
-        constexpr unsigned long long kAhead = 2;
-        const unsigned long long max_evals = (unsigned long long)std::max(cfg->max_iterations, 0) + 1;
-        unsigned long long queued = 0;
-        auto enqueue = [&]() -> int {
-            int rc = acm::normal_equations_impl(cam, n, points_3d, layout, points_2d,
-                                                cfg->invalid_policy, d_res, workspace, ne_ws,
-                                                stream, nullptr, 0, d_par, d_done, nullptr);
-            if (rc) return rc;
-            return acm::lm_step_launch(P, d_st, *cfg, d_res, d_par, d_done, hflag, ++queued,
-                                       stream);
-        };
-        int rc = ACM_SUCCESS;
-        while (queued < max_evals) {
-            // keep at most kAhead evaluations in flight; stop at the end
-            bool done = false;
-            for (unsigned spin = 1;; ++spin) {
-                const unsigned long long got = __atomic_load_n(hflag, __ATOMIC_ACQUIRE);
-                done = __atomic_load_n(hflag + 1, __ATOMIC_ACQUIRE) != 0;
-                if (done || got + kAhead > queued) break;
-                if ((spin & 255) == 0) {
-                    const hipError_t q = hipStreamQuery(s);
-                    if (q == hipSuccess) {
-                        if (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) + kAhead > queued ||
-                            __atomic_load_n(hflag + 1, __ATOMIC_ACQUIRE))
-                            continue;
-                        return sfail(ACM_ERR_HIP, "LM: step count not published");
-                    }
-                    if (q != hipErrorNotReady) return sfail(ACM_ERR_HIP, "LM: stream failed");
-                }
-                __builtin_ia32_pause();
-            }
-            if (done) break;
-            if ((rc = enqueue())) return rc;
-        }
-        if (hip_ok(hipMemcpyAsync(&st, d_st, sizeof(st), hipMemcpyDeviceToHost, s)) ||
-            hip_ok(hipStreamSynchronize(s)))
-            return sfail(ACM_ERR_HIP, "LM: device state download failed");
-    } else {
-        std::vector<double> res(R);
-        int r = acm::lm::NEED_EVAL;
-        while (r == acm::lm::NEED_EVAL) {
-            int rc = eval(st.xn, res.data());
-            if (rc) return rc;
-            r = acm::lm::consume(st, *cfg, res.data(), P);
-        }
+    // the host loop: one normal-equations evaluation per state-machine step
+    // (lm_core.hpp).  A device-resident form of this loop (r04: the state
+    // machine in a one-wave kernel behind each evaluation, the host queueing
+    // evaluations ahead) measured slower -- 1.41 vs 1.33 ms at config 3 --
+    // and was removed in r05 (history: git show 5cd4fce:apex-camera-models_amd/csrc/solver.hip).
+    std::vector<double> res(R);
+    int r = acm::lm::NEED_EVAL;
+    while (r == acm::lm::NEED_EVAL) {
+        int rc = eval(st.xn, res.data());
+        if (rc) return rc;
+        r = acm::lm::consume(st, *cfg, res.data(), P);
     }
     for (int i = 0; i < P; ++i) cam->params[i] = st.x[i];
     acm_lm_summary sum;

@@ -24,6 +24,14 @@ in the same run, and the north-star collective -- one RCCL all-reduce of
 (sum ||r||^2, n_valid) of a residual pass over each rank's shard -- timed on
 its own.  Timing is barrier + synchronize on both sides and the max over
 ranks; rank 0 prints ONE JSON line.
+
+Robustness (r05): the process group is created with a bounded timeout and
+every phase (init, the device census, the timed steps, each collective,
+each BASELINE leg) runs under a per-rank watchdog (ACM_BENCH_TIMEOUT, 120 s
+default): a rank that hangs exits 124 naming its rank, LOCAL_RANK and
+device, and the launcher stops the others.  The line records every rank's
+device (`ranks_devices`).  A BASELINE leg that raises is reported as
+{"error": ...} in its sub-object; the headline line is printed regardless.
 """
 import argparse
 import ctypes
@@ -317,6 +325,65 @@ def launch_ranks(n):
     return rc
 
 
+class PhaseWatchdog:
+    """One per rank: bounds every phase of the run (process-group init, the
+    timed steps, each collective, each BASELINE leg) so that a rank stuck in
+    an RCCL collective -- e.g. on the first 8-GPU run -- ends the job within
+    the bound instead of at the driver's limit, with a message naming the
+    rank, its LOCAL_RANK and device ordinal.  A daemon thread polls the
+    armed deadline; on expiry it prints and leaves with os._exit(124) (the
+    launcher -- launch_ranks or torchrun -- then stops the other ranks)."""
+
+    def __init__(self, rank, local, device, seconds):
+        import threading
+        self.rank, self.local, self.device, self.seconds = rank, local, device, seconds
+        self.phase, self.deadline = None, None
+        self._lock = threading.Lock()
+        threading.Thread(target=self._run, daemon=True, name="bench-watchdog").start()
+
+    def arm(self, phase, seconds=None):
+        with self._lock:
+            self.phase = phase
+            self.deadline = time.monotonic() + (seconds or self.seconds)
+
+    def disarm(self):
+        with self._lock:
+            self.phase, self.deadline = None, None
+
+    def who(self):
+        return f"rank {self.rank} (LOCAL_RANK {self.local}, device {self.device})"
+
+    def _run(self):
+        while True:
+            time.sleep(0.25)
+            with self._lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                phase = self.phase
+            if late:
+                print(f"bench.py: {self.who()} did not finish '{phase}' within "
+                      f"{self.seconds:.0f} s; exiting", file=sys.stderr, flush=True)
+                os._exit(124)
+
+
+def run_legs(want, runners, wd=None):
+    """The BASELINE legs after the headline's timed region: each leg's result,
+    or {"error": ...} when it raised -- a failing leg never costs the
+    already measured headline line.  runners: [(key, name, fn)]."""
+    legs = {}
+    for key, name, fn in runners:
+        if key not in want:
+            continue
+        if wd:
+            wd.arm(f"leg {name}")
+        try:
+            legs[name] = fn()
+        except Exception as e:  # noqa: BLE001 -- reported in the line
+            legs[name] = {"error": f"{type(e).__name__}: {e}"[:500]}
+            print(f"bench.py: leg {name} failed: {legs[name]['error']}", file=sys.stderr,
+                  flush=True)
+    return legs
+
+
 class LegCtx:
     """What the BASELINE config-4/5 legs need of the run: rank, world, the
     process group (None at N = 1) and the device of the collectives'
@@ -542,21 +609,58 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # Rehearsal knobs for a 1-GPU box (never set by the driver): run every
-    # rank on device 0 and/or use gloo for the timing barrier/all-reduce.
+    # Rehearsal knobs (never set by the driver): run every rank on device 0
+    # and/or use gloo for the timing barrier/all-reduce on a 1-GPU box;
+    # ACM_BENCH_CPU_REHEARSAL=1 (tests on a GPU-less host) stops after the
+    # process-group init and the device census, touching no GPU.
     if os.environ.get("ACM_BENCH_SAME_DEVICE") == "1":
         local = 0
     backend = os.environ.get("ACM_BENCH_BACKEND", "nccl")
+    rehearsal = os.environ.get("ACM_BENCH_CPU_REHEARSAL") == "1"
+    # every phase (init, timed steps, each collective, each leg) is bounded
+    tmo = float(os.environ.get("ACM_BENCH_TIMEOUT", "120"))
+    device = None if rehearsal else (local if world > 1 else 0)
+    wd = PhaseWatchdog(rank, local, device, tmo)
+    global _WD
+    _WD = wd
+    wd.arm("process-group init")
     if world > 1:
-        torch.cuda.set_device(local)
+        from datetime import timedelta
+        if not rehearsal:
+            torch.cuda.set_device(local)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    timeout=timedelta(seconds=tmo))
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timedelta(seconds=tmo))
         world = dist.get_world_size()
         rank = dist.get_rank()
-    else:
+        wd.rank = rank
+    elif not rehearsal:
         torch.cuda.set_device(0)
+    # which device every rank runs on, recorded in the line (a first 8-GPU
+    # run that maps two ranks to one device shows up here)
+    wd.arm("device census")
+    me = {"rank": rank, "local_rank": local, "device": device}
+    if device is not None:
+        pr = torch.cuda.get_device_properties(device)
+        me["pci"] = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+    ranks_devices = [me]
+    if world > 1:
+        ranks_devices = [None] * world
+        withhold = os.environ.get("ACM_BENCH_WITHHOLD_RANK")  # tests: a rank that never joins
+        if withhold is not None and int(withhold) == rank:
+            time.sleep(10 * tmo)
+        dist.all_gather_object(ranks_devices, me)
+    if rehearsal:
+        wd.disarm()
+        if rank == 0:
+            print(json.dumps({"rehearsal": "cpu", "n_ranks_seen": world,
+                              "ranks_devices": ranks_devices}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    wd.arm("setup")
     dev = torch.device("cuda", torch.cuda.current_device())
     cdev = dev if backend == "nccl" else torch.device("cpu")  # collectives' tensors
 
@@ -666,15 +770,18 @@ def main():
             ok = ok and torch.equal(jc.view(torch.int64), j1.cpu().view(torch.int64))
         return bool(ok)
 
+    wd.arm(f"{a.scaling}-scaling timed steps")
     main_res, (pts, n) = measure(a.scaling)
     other = None
     if world > 1:  # the other scaling mode, same process group, same run
         del pts
         other_mode = "strong" if a.scaling == "weak" else "weak"
+        wd.arm(f"{other_mode}-scaling timed steps")
         other, _ = measure(other_mode)
         other["mode"] = other_mode
         pts, n, _ = points(a.scaling)  # the residual pass below runs on the primary shard
 
+    wd.arm("residual pass + all-reduce")
     # The north-star collective: per rank one residual pass over its shard
     # (acm_reprojection_stats against observations projected with fx * 1.01),
     # then ONE all-reduce of (sum ||r||^2, n_valid) -- timed on its own.
@@ -725,16 +832,16 @@ def main():
 
     # BASELINE configs 4 and 5 (the multi-GPU configs), after the headline's
     # timed region and its collective: sub-objects of the one line
-    legs = {}
     want_legs = set() if a.legs == "none" else set(a.legs.split(","))
+    legs = {}
     if want_legs:
         del pts, obs, sto, pts_aos
         torch.cuda.empty_cache()
         ctx = LegCtx(rank, world, dist if world > 1 else None, cdev)
-        if "4" in want_legs:
-            legs["config4"] = leg_config4(ctx, a.leg4_points, a.leg_steps)
-        if "5" in want_legs:
-            legs["config5"] = leg_config5(ctx, a.leg5_cells)
+        legs = run_legs(want_legs, [("4", "config4",
+                                     lambda: leg_config4(ctx, a.leg4_points, a.leg_steps)),
+                                    ("5", "config5", lambda: leg_config5(ctx, a.leg5_cells))], wd)
+        torch.cuda.empty_cache()
 
     if rank == 0:
         bpp = 24 + 16 + 1 + (16 * P if want_j else 0)
@@ -772,12 +879,14 @@ def main():
                          "algorithmic_bytes_per_launch": bpp * main_res["points_per_rank"],
                          "kernel_ms": kern_ms},
             "collective": coll,
+            "ranks_devices": ranks_devices,
         }
         if "shards_match_single_projection" in main_res:
             out["shards_match_single_projection"] = main_res["shards_match_single_projection"]
         if other is not None:
             out[other["mode"]] = other
         out.update(legs)
+        wd.arm("cpu baseline", 10 * tmo)
         if not a.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             out["cpu_baseline"] = cpu_baseline(model_id, params, w, h, main_res["points_per_rank"],
                                                a.cpu_baseline_seconds)
@@ -790,10 +899,19 @@ def main():
                     model_id, params, w, h, main_res["points_per_rank"],
                     a.cpu_baseline_seconds / 2, thr)
         print(json.dumps(out), flush=True)
+    wd.arm("shutdown")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    wd.disarm()
 
+
+_WD = None
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception:
+        if _WD is not None:  # name the rank and the phase that raised
+            print(f"bench.py: {_WD.who()} failed in '{_WD.phase}'", file=sys.stderr, flush=True)
+        raise

@@ -534,12 +534,17 @@ ACM_API int acm_stream_synchronize(void *stream);
  * 16-B aligned; 1 / 2 = pixels per lane with three 8-B stores per ray; 3 =
  * 1 pixel per lane, staged when rays is 16-B aligned).
  * Outputs are identical for every value.
- * ACM_TUNE_LM_DEVICE (r04): acm_lm_optimize without an all-reduce callback
- * keeps the LM's state on the device -- a one-thread step kernel behind each
- * evaluation's normal equations computes the next trial point, and the host
- * only keeps two evaluations queued ahead -- instead of a host round trip
- * per evaluation: -1 = auto = on, 0 = the host loop, 1 = on.  The same
- * state machine (lm_core.hpp) either way: bit-identical iterates.
+ * ACM_TUNE_LM_DEVICE (16): removed in round 5.  Round 4 added it to run the
+ * LM state machine on the device behind each evaluation; that loop measured
+ * slower than the host loop (1.41 vs 1.33 ms at config 3) and never was the
+ * default.  acm_set_tuning returns ACM_ERR_NOT_SUPPORTED; acm_lm_optimize
+ * always runs the host loop.
+ * Defaults (the value acm_set_tuning returns as "previous" in a fresh
+ * process; tests/test_capi.py checks every one): PROJECT_VARIANT -1,
+ * RESIDUAL_NT 0, NE_WAVES 0, FOV_UNROLL -1, NE_UNROLL 0, ALIGN_J -1,
+ * NT_LOADS -1, NT_LOADS_UNPROJECT -1, LM_HOST_RESULT -1, SAMPLE_FUSED -1,
+ * UNPROJECT_RCP -1, SAMPLE_PATIENCE -1, UNPROJECT_PPT -1, SAMPLE_CERT -1,
+ * SAMPLE_WRITE -1.
  * Every knob is an atomic: acm_set_tuning may race with any other call.
  * Returns the previous value or an error. */
 enum {

@@ -65,11 +65,22 @@ def size_classes(durs, ratio=1.5):
     return cls
 
 
+def waves_per_simd(r):
+    """register-limited waves per SIMD (512 VGPRs + AGPRs per lane-slot on
+    CDNA3/4 in 8-register granules, at most 8 waves), ignoring LDS"""
+    v = r["vgprs"] + r["agprs"]
+    if v <= 0:
+        return None
+    v = (v + 7) // 8 * 8
+    return min(8, 512 // v)
+
+
 def durations(kt_dir):
     """(short name, grid size, size class) -> {calls, avg_us, min_us} from the
     per-dispatch kernel trace (the --stats table aggregates over launch
     sizes), plus the occurrence -> class map of every (name, grid)."""
     acc = collections.defaultdict(list)
+    res = {}
     for r in csv.DictReader(open(os.path.join(kt_dir, "kt_kernel_trace.csv"))):
         if "acm::" not in r["Kernel_Name"]:
             continue
@@ -77,6 +88,10 @@ def durations(kt_dir):
         acc[(short(r["Kernel_Name"]), grid)].append(
             (int(r["Dispatch_Id"]),
              (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+        res[(short(r["Kernel_Name"]), grid)] = {
+            "vgprs": int(r.get("VGPR_Count") or 0), "agprs": int(r.get("Accum_VGPR_Count") or 0),
+            "sgprs": int(r.get("SGPR_Count") or 0), "lds_bytes": int(r.get("LDS_Block_Size") or 0),
+            "block": int(r.get("Workgroup_Size_X") or 0)}
     out, classes = {}, {}
     for k, v in acc.items():
         v.sort()
@@ -85,7 +100,8 @@ def durations(kt_dir):
         classes[k] = cls
         for c in set(cls):
             ds = [d for d, ci in zip(durs, cls) if ci == c]
-            out[k + (c,)] = {"calls": len(ds), "avg_us": sum(ds) / len(ds), "min_us": min(ds)}
+            out[k + (c,)] = {"calls": len(ds), "avg_us": sum(ds) / len(ds), "min_us": min(ds),
+                             **res[k], "waves_per_simd_max": waves_per_simd(res[k])}
     return out, classes
 
 
@@ -178,9 +194,9 @@ def summarize(dur, ctr):
 
 
 def table(out):
-    lines = ["| kernel | grid | calls | avg us | VALU busy | VALU inst/wave | FP64 TF (frac) | "
-             "HBM GB/s (frac) | TA busy | TD busy | wait / issue-stall / active |",
-             "|---|---|---|---|---|---|---|---|---|---|---|"]
+    lines = ["| kernel | grid | calls | avg us | VGPR (waves/SIMD) | VALU busy | VALU inst/wave | "
+             "FP64 TF (frac) | HBM GB/s (frac) | TA busy | TD busy | wait / issue-stall / active |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|"]
     f = lambda x, fmt: (fmt % x) if x is not None else "-"  # noqa: E731
     for _, r in sorted(out.items(), key=lambda kv: -kv[1].get("avg_us", 0)):
         hbm = f(r.get("hbm_GBps"), "%.0f") + f" ({f(r.get('hbm_frac_of_peak'), '%.2f')})"
@@ -194,7 +210,8 @@ def table(out):
         lines.append(
             f"| {r['kernel']} | {r['grid_size']}"
             f"{'' if r['size_class'] == 0 else ' #%d' % r['size_class']} | {r.get('calls', '-')} | "
-            f"{f(r.get('avg_us'), '%.1f')} | {f(r.get('valu_busy'), '%.2f')} | "
+            f"{f(r.get('avg_us'), '%.1f')} | {r.get('vgprs', '-')} "
+            f"({r.get('waves_per_simd_max', '-')}) | {f(r.get('valu_busy'), '%.2f')} | "
             f"{f(r.get('valu_insts_per_wave'), '%.0f')} | {fp} | {hbm} | "
             f"{f(r.get('ta_busy'), '%.2f')} | {f(r.get('td_busy'), '%.2f')} | "
             f"{f(r.get('wait_any_share'), '%.2f')} / {f(r.get('wait_inst_share'), '%.2f')} / "

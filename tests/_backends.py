@@ -54,6 +54,18 @@ class GpuBackend:
         return (uv.cpu().numpy(), st.cpu().numpy(),
                 jac.cpu().numpy() if jac is not None else None)
 
+    def round_trip(self, model, params, w, h, pts, layout="aos"):
+        """acm_project_unproject: (uv, status, rays (N,3), ray_status)"""
+        m = self._model(model, params, w, h)
+        pts = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 3)
+        t = self.torch.as_tensor(pts if layout == "aos" else pts.T.copy(), device="cuda")
+        uv, st, rays, st2 = m.project_unproject_batch(t, layout=layout)
+        self.torch.cuda.synchronize()
+        r = rays.cpu().numpy()
+        if layout == "soa":
+            r = r.T.copy()
+        return uv.cpu().numpy(), st.cpu().numpy(), r, st2.cpu().numpy()
+
     def unproject(self, model, params, w, h, uv, layout="aos", reference_newton=False):
         m = self._model(model, params, w, h)
         t = self.torch.as_tensor(np.ascontiguousarray(uv, dtype=np.float64).reshape(-1, 2),

@@ -142,3 +142,77 @@ def test_parent_sigkill_stops_ranks(tmp_path):
     p.send_signal(signal.SIGKILL)
     p.wait(timeout=30)
     assert _gone(pids), pids
+
+
+def _tagged_pids(tag):
+    """pids of live (non-zombie) processes whose environment carries tag"""
+    out = []
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/environ", "rb") as f:
+                if f"ACM_TEST_TAG={tag}".encode() not in f.read():
+                    continue
+            with open(f"/proc/{d}/stat") as f:
+                if f.read().split(")")[-1].split()[0] == "Z":
+                    continue
+        except (FileNotFoundError, PermissionError, ProcessLookupError):
+            continue
+        out.append(int(d))
+    return out
+
+
+def test_cpu_rehearsal_device_census_world2():
+    """`bench.py --gpus 2` on gloo up to the device census (no GPU touched):
+    both ranks join within the bounded init and rank 0's line records every
+    rank's (rank, LOCAL_RANK, device)"""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2"],
+                       env=_env(ACM_BENCH_BACKEND="gloo", ACM_BENCH_CPU_REHEARSAL="1",
+                                ACM_BENCH_TIMEOUT="60"),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    import json
+    d = json.loads(lines[0])
+    assert d["n_ranks_seen"] == 2
+    assert [(x["rank"], x["local_rank"]) for x in d["ranks_devices"]] == [(0, 0), (1, 1)]
+
+
+def test_withheld_collective_exits_within_bound():
+    """one rank never joins the first collective; the job
+    ends non-zero within the bound (ACM_BENCH_TIMEOUT = 5 s, not the
+    driver's 600 s), stderr names the rank, no line is printed and no rank
+    process outlives the parent"""
+    import time
+    import uuid
+    tag = uuid.uuid4().hex
+    t0 = time.time()
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2"],
+                       env=_env(ACM_BENCH_BACKEND="gloo", ACM_BENCH_CPU_REHEARSAL="1",
+                                ACM_BENCH_TIMEOUT="5", ACM_BENCH_WITHHOLD_RANK="1",
+                                ACM_TEST_TAG=tag),
+                       capture_output=True, text=True, timeout=300)
+    dt = time.time() - t0
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "LOCAL_RANK" in r.stderr and "device census" in r.stderr, r.stderr[-2000:]
+    # 5 s bound + interpreter / torch import time of the ranks
+    assert dt < 120, dt
+    assert _gone(_tagged_pids(tag)), _tagged_pids(tag)
+
+
+def test_failing_leg_keeps_the_headline():
+    """a BASELINE leg that raises becomes {"error": ...} in its
+    sub-object; the legs after it still run (the headline line is built from
+    run_legs' result, so it is printed either way)"""
+    import bench
+
+    def boom():
+        raise MemoryError("HIP out of memory")
+    legs = bench.run_legs({"4", "5"}, [("4", "config4", boom),
+                                       ("5", "config5", lambda: {"value": 1.0})])
+    assert legs["config4"]["error"].startswith("MemoryError")
+    assert legs["config5"] == {"value": 1.0}
+    assert bench.run_legs(set(), [("4", "config4", boom)]) == {}

@@ -177,6 +177,36 @@ def test_tuning_knobs_validate_and_restore():
     assert L.acm_set_tuning(99, 0) == _lib.ERR_INVALID_ARGUMENT
     # numerics are per call since round 3: the old process-wide knob is gone
     assert L.acm_set_tuning(_lib.TUNE_NEWTON_FAST, 0) == _lib.ERR_NOT_SUPPORTED
+    # the device-resident LM (r04) is gone since round 5
+    assert L.acm_set_tuning(16, 1) == _lib.ERR_NOT_SUPPORTED
+
+
+def test_tuning_defaults_match_the_header():
+    """every knob's default, read in a fresh process as
+    the previous value acm_set_tuning returns, equals the one include/acm.h
+    documents (its "Defaults (...)" list; r04's header called
+    ACM_TUNE_LM_DEVICE's -1 "on" while the code took it as off)."""
+    import subprocess
+    import sys
+    text = open(os.path.join(ROOT, "include", "acm.h")).read()
+    block = re.search(r"Defaults \(the value acm_set_tuning returns.*?\):(.*?)\.\n", text,
+                      re.S).group(1)
+    documented = {k: int(v) for k, v in re.findall(r"([A-Z_]+) (-?\d+)", block)}
+    keys = dict(re.findall(r"ACM_TUNE_([A-Z_]+) = (\d+)", text))
+    removed = {"NEWTON_FAST", "LM_DEVICE"}
+    assert set(documented) == set(keys) - removed, (set(documented) ^ (set(keys) - removed))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from apex_camera_models import _lib\n"
+            "L = _lib.load()\n"
+            "for k, d in %r:\n"
+            "    print(k, L.acm_set_tuning(k, d))\n") % (
+                os.path.join(ROOT, "apex-camera-models_amd"),
+                sorted((int(keys[name]), d) for name, d in documented.items()))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         check=True, timeout=300).stdout
+    got = {int(a): int(b) for a, b in (ln.split() for ln in out.splitlines())}
+    for name, default in documented.items():
+        assert got[int(keys[name])] == default, (name, got[int(keys[name])], default)
 
 
 def test_newton_tolerance_threshold_is_exact():

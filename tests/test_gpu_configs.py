@@ -74,37 +74,36 @@ def test_config3_kb_to_ds_conversion_9m():
 
 @pytest.mark.parametrize("model", range(6))
 def test_config4_round_trip_6_25m(model):
-    """BASELINE config 4 at its own per-GPU size: project -> unproject of
-    6.25M synthetic points (the bench distribution, 0.1% edge points) for
-    each of the six north-star models.  Statuses of both steps bit-exact
-    against the oracle on a strided 200k subsample (the oracle unprojects
-    the GPU's own pixels), uv / rays within 1e-10 there; over all 6.25M
-    points the round trip preserves the direction the way
+    """BASELINE config 4 at its own per-GPU size: the project -> unproject
+    round trip of 6.25M synthetic points (the bench distribution, 0.1% edge
+    points) for each of the six north-star models, through the fused entry
+    the bench leg times (acm_project_unproject).  On a strided 200k
+    subsample both statuses are bit-exact against the oracle's project
+    followed by its unproject of its own pixels, uv / rays within 1e-10,
+    values bit-exact for the models without a transcendental
+    (test_gpu_parity.check_round_trip_vs_oracle); over all 6.25M points the
+    round trip preserves the direction the way
     tests/projection_accuracy.rs:49-74 asserts (|dot - 1| < 1e-6) -- except
     UCM, whose reference unprojection keeps the 1 - r^2 quirk (ucm.rs:354):
     there the GPU round trip equals the oracle's on the subsample instead."""
     import torch
     from apex_camera_models import samples
     from apex_camera_models.camera import MODEL_CLASSES, Resolution
+    from test_gpu_parity import check_round_trip_vs_oracle
     names = {0: "pinhole", 1: "rad_tan", 2: "kannala_brandt", 3: "double_sphere", 4: "ucm",
              5: "eucm"}
     n = 6_250_000
     params, (w, h) = samples.SAMPLES[model]
     m = MODEL_CLASSES[names[model]]._from_params(list(params), Resolution(w, h))
-    pts = samples.synthetic_points_device(n, offset=3 * n)  # rank 3's shard
-    uv, st, _ = m.project_batch(pts)
-    ray, st2 = m.unproject_batch(torch.where(torch.isnan(uv), torch.zeros_like(uv), uv))
+    # rank 3's shard of config 4's 50M-point global batch, as the bench leg slices it
+    lo = 3 * n
+    pts = samples.synthetic_points_device(8 * n)[lo:lo + n].contiguous()
+    uv, st, ray, st2 = m.project_unproject_batch(pts)
     torch.cuda.synchronize()
     sub = torch.arange(0, n, n // 200_000, device="cuda")
-    p_h = pts[sub].cpu().numpy()
-    uv0, s0, _ = O.project(model, params, w, h, p_h)
-    assert np.array_equal(st[sub].cpu().numpy(), s0)
-    assert rel_err(uv[sub].cpu().numpy(), uv0, floor=1.0) <= 1e-10
-    uv_g = uv[sub].cpu().numpy()
-    uv_in = np.where(np.isnan(uv_g), 0.0, uv_g)
-    r0, s20 = O.unproject(model, params, w, h, uv_in)
-    assert np.array_equal(st2[sub].cpu().numpy(), s20)
-    assert rel_err(ray[sub].cpu().numpy(), r0, floor=1.0) <= 1e-10
+    check_round_trip_vs_oracle(model, params, w, h, pts[sub].cpu().numpy(),
+                               uv[sub].cpu().numpy(), st[sub].cpu().numpy(),
+                               ray[sub].cpu().numpy(), st2[sub].cpu().numpy())
     ok = (st == 0) & (st2 == 0) & torch.isfinite(pts).all(1)
     assert int(ok.sum()) > 0.8 * n
     pn = pts[ok] / torch.linalg.norm(pts[ok], dim=1, keepdim=True)

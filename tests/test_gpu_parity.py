@@ -853,3 +853,39 @@ def test_project_unproject_fused_matches_two_calls(model, n, layout):
     for x, y in zip(a, b):
         xh, yh = x.cpu().numpy(), y.cpu().numpy()
         assert xh.tobytes() == yh.tobytes() or np.array_equal(xh, yh, equal_nan=True)
+
+
+def check_round_trip_vs_oracle(model, params, w, h, xyz, uv, st, rays, st2):
+    """acm_project_unproject's four outputs against the oracle's project of the
+    same points followed by the oracle's unproject of the ORACLE's own pixels
+    (NaN pixels of failed projections included), the per-point loop of
+    tests/projection_accuracy.rs:49-73 over mod.rs:256 / :271.  Statuses of
+    both steps bit-exact; uv and rays within 1e-10 (floor 1); bit-exact values
+    for the models without a transcendental (pixels: Pinhole, RadTan, DS, UCM,
+    EUCM; rays: Pinhole, DS, UCM, EUCM), RadTan rays within 8 ulp of 1."""
+    uv0, s0, _ = O.project(model, params, w, h, xyz)
+    assert np.array_equal(st, s0), np.nonzero(st != s0)[0][:5]
+    assert rel_err(uv, uv0, floor=1.0) <= TOL
+    if model in NO_TRANSCENDENTAL_PROJECT:
+        assert np.array_equal(uv, uv0, equal_nan=True)
+    r0, s20 = O.unproject(model, params, w, h, uv0)
+    assert np.array_equal(st2, s20), np.nonzero(st2 != s20)[0][:5]
+    assert rel_err(rays, r0, floor=1.0) <= TOL
+    if model in EXACT_RAYS_UNPROJECT:
+        assert np.array_equal(rays, r0, equal_nan=True)
+    if model == 1:
+        assert ulps_of_one(rays[s20 == 0], r0[s20 == 0]) <= 8
+
+
+@pytest.mark.parametrize("layout", ["aos", "soa"])
+@pytest.mark.parametrize("model", range(7))
+def test_project_unproject_fused_vs_oracle_golden(be, golden_dir, model, layout):
+    """acm_project_unproject on every golden point set (edge points on every
+    decision boundary, z <= 0, the origin, non-finite coordinates), pinned to
+    the oracle directly (VERDICT r04 next 1), not only to the two-call path;
+    its pixels and statuses also equal the frozen golden ones."""
+    g, params, w, h = _golden(golden_dir, model)
+    uv, st, rays, st2 = be.round_trip(model, params, w, h, g["xyz"], layout=layout)
+    assert np.array_equal(st, g["proj_status"])
+    assert rel_err(uv, g["uv"], floor=1.0) <= TOL
+    check_round_trip_vs_oracle(model, params, w, h, g["xyz"], uv, st, rays, st2)

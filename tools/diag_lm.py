@@ -1,9 +1,9 @@
 """LM loop overhead on config-3 data (KB-sampled correspondences, DS target):
 wall time of acm_lm_optimize vs evaluations x the normal-equation kernel
-time, i.e. the host / launch / copy cost per evaluation, for the
-device-resident loop (ACM_TUNE_LM_DEVICE, r04: "dev") and the host loop with
-each ACM_TUNE_LM_HOST_RESULT mode (0 copy + sync, 1 pinned + sync, 2 pinned
-+ spin on the completion word); the reported wall is the default.
+time, i.e. the host / launch / copy cost per evaluation, for the host loop
+with each ACM_TUNE_LM_HOST_RESULT mode (0 copy + sync, 1 pinned + sync, 2
+pinned + spin on the completion word); the reported wall is the default (2).
+(r04 also timed a device-resident loop here; it was removed in r05.)
 
   python tools/diag_lm.py [--points N]
 """
@@ -50,10 +50,9 @@ def main():
     L = _lib.load()
     by_mode = {}
     res = None
-    modes = {"dev": (1, -1), "host0": (0, 0), "host1": (0, 1), "host2": (0, 2)}
+    modes = {"host0": 0, "host1": 1, "host2": 2}
     for _ in range(3):
-        for mode, (dev, host) in modes.items():
-            L.acm_set_tuning(_lib.TUNE_LM_DEVICE, dev)
+        for mode, host in modes.items():
             L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, host)
             m = conversion._init_target("double_sphere", src)
             m._set_params(list(p0))
@@ -65,8 +64,7 @@ def main():
             ms = (time.perf_counter() - t0) * 1e3
             by_mode[mode] = min(by_mode.get(mode, 1e9), ms)
     L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, -1)
-    L.acm_set_tuning(_lib.TUNE_LM_DEVICE, -1)
-    wall = by_mode["dev"]
+    wall = by_mode["host2"]
     print(json.dumps({"what": "LM loop overhead", "points": n, "lm_wall_ms": round(wall, 3),
                       "lm_wall_ms_by_mode": {k: round(v, 3) for k, v in by_mode.items()},
                       "evaluations": res.evaluations, "iterations": res.iterations,

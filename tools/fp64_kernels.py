@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--points", type=int, default=10_000_000)
     ap.add_argument("--cells", type=int, default=100_000_000)
+    ap.add_argument("--rt-points", type=int, default=50_000_000,
+                    help="points of the rt_* (config-4 round trip) kernels")
     ap.add_argument("--sample-fused", type=int, default=None,
                     help="ACM_TUNE_SAMPLE_FUSED for sample_kb (-1 auto = segment path, 0 two-pass, 1/2/3 = single pass R 2/4/8)")
     ap.add_argument("--lib", default=None, help="load this libacm build instead (A/B builds, "
@@ -82,6 +84,29 @@ def main():
                                            0, st.data_ptr(), sh))
         emit(name, n, ms, 41)
         del uv, rays, st
+    # config 4's fused round trip (acm_project_unproject) at the bench leg's
+    # 50M points on one GPU: rt_pinhole, rt_radtan, rt_kb, rt_ds, rt_ucm, rt_eucm
+    rt = [(mid, nm) for mid, nm in ((0, "rt_pinhole"), (1, "rt_radtan"), (2, "rt_kb"),
+                                    (3, "rt_ds"), (4, "rt_ucm"), (5, "rt_eucm")) if nm in want]
+    if rt:
+        del pts
+        m = a.rt_points
+        p50 = samples.synthetic_points_device(m)
+        uv = torch.empty((m, 2), dtype=torch.float64, device="cuda")
+        st = torch.empty((m,), dtype=torch.uint8, device="cuda")
+        rays = torch.empty((m, 3), dtype=torch.float64, device="cuda")
+        st2 = torch.empty((m,), dtype=torch.uint8, device="cuda")
+        for mid, name in rt:
+            params, (w, h) = samples.SAMPLES[mid]
+            cam = _lib.AcmCamera()
+            _lib.check(L.acm_camera_init(ctypes.byref(cam), mid, (ctypes.c_double * len(params))(
+                *params), len(params), w, h))
+            ms = timed(lambda: _lib.check(L.acm_project_unproject(
+                ctypes.byref(cam), m, p50.data_ptr(), 0, uv.data_ptr(), st.data_ptr(),
+                rays.data_ptr(), st2.data_ptr(), sh)))
+            emit(name, m, ms, 66)
+        del p50, uv, st, rays, st2
+        pts = samples.synthetic_points_device(n)
     if "kb_normal_eq" in want:
         p2 = pts[torch.isfinite(pts).all(1)].contiguous()
         params, (w, h) = samples.SAMPLES[2]
