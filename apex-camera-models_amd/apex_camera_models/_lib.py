@@ -74,6 +74,7 @@ TUNE_UNPROJECT_PPT = 13
 TUNE_SAMPLE_CERT = 14
 TUNE_SAMPLE_WRITE = 15
 TUNE_LM_DEVICE = 16  # removed in r05 (acm_set_tuning: ACM_ERR_NOT_SUPPORTED)
+TUNE_ROUND_TRIP = 17  # r05: acm_project_unproject PPT + 8 x ray stores (same outputs)
 ERR_NOT_SUPPORTED = -6
 ERR_NUMERICAL = -7
 LM_TERMINATION = {0: "MaxIterations", 1: "CostTolerance", 2: "ParameterTolerance",

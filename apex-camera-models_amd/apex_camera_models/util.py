@@ -115,13 +115,14 @@ def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d) 
     p3 = _as_device_f64(points3d, 3)
     p2 = _as_device_f64(points2d, 2)
     n = p3.shape[0]
-    if p2.shape[0] != n:
-        raise ValueError("points3d and points2d must have the same number of columns")
+    if p2.shape[0] != n:  # as linear_estimation raises it (kannala_brandt.rs:168-172 & co)
+        raise InvalidParams("Number of 2D and 3D points must match")
     ws_bytes = L.acm_linear_estimation_with_error_workspace_size(model.MODEL_ID, n)
     if ws_bytes == 0:
         raise InvalidParams(f"{model.NAME} has no GPU linear_estimation")
     ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=p3.device)
-    res = torch.empty((9,), dtype=torch.float64, device=p3.device)
+    # NaN until written: an early error return of the C call leaves it so
+    res = torch.full((9,), float("nan"), dtype=torch.float64, device=p3.device)
     cam = model.acm_camera()
     rc = L.acm_linear_estimation_with_error(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
                                             p2.data_ptr(), res.data_ptr(), ws.data_ptr(),
@@ -129,6 +130,10 @@ def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d) 
     if rc not in (_lib.ACM_SUCCESS, _lib.ERR_INVALID_PARAMS, _lib.ERR_NUMERICAL):
         _lib.check(rc)
     out = res.cpu().tolist()
+    if out[5] != out[5]:  # the initial error was never computed: the call's own error
+        if rc == _lib.ERR_NUMERICAL:
+            raise NumericalError(_lib.last_error())
+        raise InvalidParams(_lib.last_error())
     n_valid = int(out[5])
     if n_valid == 0:
         raise ZeroProjectionPoints()

@@ -315,6 +315,10 @@ static std::atomic<int> g_sample_patience{-1};
 // point: -1 = auto = on, 0 = off, 1 = on.
 static std::atomic<int> g_unproject_rcp{-1};
 static std::atomic<int> g_unproject_ppt{-1};
+// acm_project_unproject's points per lane and AoS ray stores (include/acm.h
+// ACM_TUNE_ROUND_TRIP): -1 = auto; else PPT (1, 2, 4) + 8 x stores (0 =
+// the model's default, 1 = LDS-staged, 2 = three 8-B stores per ray).
+static std::atomic<int> g_round_trip{-1};
 // acm_lm_optimize without an all-reduce: the normal-equations epilogue writes
 // its P*P + P + 2 results straight into pinned host memory instead of device
 // memory + a device-to-host copy.  0 = off (copy + stream synchronise), 1 =
@@ -677,7 +681,9 @@ __global__ __launch_bounds__(kBlock) void k_round_trip(CamArg cam, size_t n,
                                                           nullptr);
             if (sp != ST_OK) u = v = __builtin_nan("");
             st2<NT>(uv + 2 * i, u, v);
+#ifndef ACM_AB_RT_NO_STATUS  // timing-only A/B build: the cost of the byte stores
             st1<NT>(pstatus + i, sp);
+#endif
             st = M::unproject(c, u, v, X, Y, Z);
             if (st != ST_OK) X = Y = Z = __builtin_nan("");
         }
@@ -704,7 +710,9 @@ __global__ __launch_bounds__(kBlock) void k_round_trip(CamArg cam, size_t n,
             st1d<NT>(rays + n + i, Y);
             st1d<NT>(rays + 2 * n + i, Z);
         }
+#ifndef ACM_AB_RT_NO_STATUS
         if (i < n) st1<NT>(rstatus + i, st);
+#endif
     }
 }
 
@@ -715,6 +723,31 @@ __global__ __launch_bounds__(kBlock) void k_round_trip(CamArg cam, size_t n,
 template <class TagT> struct UnprojectStaged { static constexpr bool on = true; };
 template <> struct UnprojectStaged<Tag<KannalaBrandt>> { static constexpr bool on = false; };
 template <> struct UnprojectStaged<Tag<RadTan>> { static constexpr bool on = false; };
+
+// acm_project_unproject's defaults per model: points per lane and whether
+// the AoS rays go out LDS-staged (ACM_TUNE_ROUND_TRIP overrides both).
+// From the r05 A/B at config 4's 50M points (tools/diag_round_trip.py,
+// profiles/r05d_round_trip_ab.log, best of 3 interleaved blocks): one point
+// per lane for Pinhole / UCM / EUCM (0.565 -> 0.553 ms) and for KB, whose
+// rays are now staged too (its VALU work fell with the SGPR-spill fix:
+// 0.608 -> 0.587); four per lane for DS (0.641 -> 0.626); RadTan keeps two,
+// direct stores (every setting within 1.5%).
+template <class TagT> struct RoundTripDefault {
+    static constexpr int ppt = 1;
+    static constexpr bool staged = true;
+};
+template <> struct RoundTripDefault<Tag<DoubleSphere>> {
+    static constexpr int ppt = 4;
+    static constexpr bool staged = true;
+};
+template <> struct RoundTripDefault<Tag<RadTan>> {
+    static constexpr int ppt = 2;
+    static constexpr bool staged = false;
+};
+template <> struct RoundTripDefault<Tag<Fov>> {  // not measured: as acm_unproject
+    static constexpr int ppt = 2;
+    static constexpr bool staged = true;
+};
 
 
 // -------------------------------------------------- residual + Jacobian
@@ -4055,22 +4088,36 @@ ACM_API int acm_project_unproject(const acm_camera* cam, size_t n, const double*
     hipStream_t s = (hipStream_t)stream;
     return dispatch_model(cam->model, [&](auto tag) -> int {
         using TagT = decltype(tag);
-        constexpr int K = 2;  // points per lane, as the unprojection
+        const int knob = g_round_trip.load(std::memory_order_relaxed);
+        const int ppt = knob < 0 ? RoundTripDefault<TagT>::ppt : (knob & 7);
+        const int smode = knob < 0 ? 0 : (knob >> 3);
         const bool nt = n * 42 > kNtThresholdBytes;
-        const bool stg = UnprojectStaged<TagT>::on && (reinterpret_cast<uintptr_t>(rays) & 15u) == 0;
-        const dim3 gk((unsigned)((n + (size_t)kBlock * K - 1) / ((size_t)kBlock * K))), b(kBlock);
-        auto go = [&](auto lay_c, auto stg_c) {
+        const bool want_stg = smode == 0 ? RoundTripDefault<TagT>::staged : smode == 1;
+        const bool stg = want_stg && (reinterpret_cast<uintptr_t>(rays) & 15u) == 0;
+        const dim3 b(kBlock);
+        auto go = [&](auto lay_c, auto ppt_c, auto stg_c) {
             constexpr int L = decltype(lay_c)::value;
+            constexpr int K = decltype(ppt_c)::value;
             constexpr bool ST = decltype(stg_c)::value && L == ACM_LAYOUT_AOS;
+            const dim3 gk((unsigned)((n + (size_t)kBlock * K - 1) / ((size_t)kBlock * K)));
             auto kern = nt ? k_round_trip<TagT, L, true, K, ST> : k_round_trip<TagT, L, false, K, ST>;
             hipLaunchKernelGGL(kern, gk, b, 0, s, prep(*cam, false), n, points_3d, points_2d,
                                status, rays, ray_status);
         };
+        using AOS = std::integral_constant<int, ACM_LAYOUT_AOS>;
+        using One = std::integral_constant<int, 1>;
+        using Two = std::integral_constant<int, 2>;
+        using Four = std::integral_constant<int, 4>;
+        auto by_ppt = [&](auto stg_c) {
+            if (ppt == 1) go(AOS{}, One{}, stg_c);
+            else if (ppt == 4) go(AOS{}, Four{}, stg_c);
+            else go(AOS{}, Two{}, stg_c);
+        };
         if (layout == ACM_LAYOUT_AOS) {
-            if (stg) go(std::integral_constant<int, ACM_LAYOUT_AOS>{}, std::true_type{});
-            else go(std::integral_constant<int, ACM_LAYOUT_AOS>{}, std::false_type{});
+            if (stg) by_ppt(std::true_type{});
+            else by_ppt(std::false_type{});
         } else {
-            go(std::integral_constant<int, ACM_LAYOUT_SOA>{}, std::false_type{});
+            go(std::integral_constant<int, ACM_LAYOUT_SOA>{}, Two{}, std::false_type{});
         }
         return check_launch("acm_project_unproject");
     });
@@ -4979,6 +5026,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_SAMPLE_CERT, &g_sample_cert, -1, 0, "value must be -1 (auto) or 0"},
         {ACM_TUNE_SAMPLE_WRITE, &g_sample_write, -1, 5, "value must be -1..5"},
         {ACM_TUNE_UNPROJECT_PPT, &g_unproject_ppt, -1, 3, "value must be -1..3"},
+        {ACM_TUNE_ROUND_TRIP, &g_round_trip, -1, 20, "value must be -1 or PPT (1, 2, 4) + 8 x stores (0..2)"},
     };
     if (key == ACM_TUNE_NEWTON_FAST)  // removed (r03): numerics are chosen per call
         return fail(ACM_ERR_NOT_SUPPORTED,
@@ -4993,6 +5041,8 @@ ACM_API int acm_set_tuning(int key, int value) {
         if (key == ACM_TUNE_NE_WAVES) ok = ok && value != 2;
         if (key == ACM_TUNE_FOV_UNROLL) ok = ok && value != 3;
         if (key == ACM_TUNE_UNPROJECT_PPT) ok = ok && value != 0;
+        if (key == ACM_TUNE_ROUND_TRIP)
+            ok = ok && (value == -1 || ((value & 7) == 1 || (value & 7) == 2 || (value & 7) == 4));
         if (!ok) return fail(ACM_ERR_INVALID_ARGUMENT, k.msg);
         return k.v->exchange(value);
     }

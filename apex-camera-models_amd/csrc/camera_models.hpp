@@ -109,15 +109,42 @@ __constant__ double kAtanO[10] = {  // odd-index coefficients c1, c3, ..., c19
 // (coefficients in constant memory: uniform s_loads into SGPRs, used as FMA
 // operands -- as literals they were materialised in 42 VGPRs, which held the
 // grid kernel at 3 waves/SIMD)
+//
+// coef_at_use (r05): the table's address passes through an empty asm with
+// an SGPR operand at every evaluation, so the s_loads of its coefficients
+// are issued there and cannot be hoisted to the kernel entry or merged with
+// another evaluation's.  Hoisted, the 21 atan and 22 sin / cos coefficients
+// stayed live in SGPRs across the whole kernel beside the camera's
+// constants, overflowed the 102 SGPRs and were spilled to VGPR lanes: every
+// evaluation then re-read them with ~20-45 v_readlane (VALU) instructions
+// (k_round_trip<KB>: 256 v_readlane + 80 v_writelane in the code, ~100 VALU
+// instructions of its ~400 per point).  Same coefficients, same operation
+// order: the results are bit-identical.
+// fma_sc: fma(a, b, c) with the coefficient c read straight from its SGPRs
+// (v_fma_f64 takes one scalar operand).  Left to itself the compiler picked
+// the two-operand v_fmac_f64 and first copied every coefficient into a VGPR
+// pair (two v_mov_b32 per Horner step).  The same single rounding as fma().
+typedef __attribute__((address_space(4))) const double coef_t;
+__device__ __forceinline__ coef_t* coef_at_use(const double* table) {
+    coef_t* p = (coef_t*)table;
+    asm volatile("" : "+s"(p));
+    return p;
+}
+__device__ __forceinline__ double fma_sc(double a, double b, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
+
 __device__ __forceinline__ double atan01(double b) {
-    const double* E = kAtanE;
-    const double* O = kAtanO;
+    coef_t* E = coef_at_use(kAtanE);
+    coef_t* O = coef_at_use(kAtanO);
     const double s = b * b, s2 = s * s;
     double pe = E[10], po = O[9];
 #pragma unroll
-    for (int k = 9; k >= 0; --k) pe = fma(pe, s2, E[k]);
+    for (int k = 9; k >= 0; --k) pe = fma_sc(pe, s2, E[k]);
 #pragma unroll
-    for (int k = 8; k >= 0; --k) po = fma(po, s2, O[k]);
+    for (int k = 8; k >= 0; --k) po = fma_sc(po, s2, O[k]);
     return b * fma(po, s, pe);
 }
 
@@ -204,11 +231,13 @@ __constant__ double kCosC[11] = {
 __device__ __forceinline__ void sincos_0_2(double t, double* sn, double* cs) {
     if (t >= 0.0 && t <= 2.0) {
         const double s = t * t;
-        double ps = kSinS[10], pc = kCosC[10];
+        coef_t* S = coef_at_use(kSinS);
+        coef_t* C = coef_at_use(kCosC);
+        double ps = S[10], pc = C[10];
 #pragma unroll
         for (int k = 9; k >= 0; --k) {
-            ps = fma(ps, s, kSinS[k]);
-            pc = fma(pc, s, kCosC[k]);
+            ps = fma_sc(ps, s, S[k]);
+            pc = fma_sc(pc, s, C[k]);
         }
         *sn = t * ps;
         *cs = pc;
@@ -221,11 +250,13 @@ __device__ __forceinline__ void sincos_0_2(float t, float* sn, float* cs) { sinc
 // t is in [0, 2] (KannalaBrandt::ray_certified: theta in [0, pi/2)).
 __device__ __forceinline__ void sincos_poly_0_2(double t, double* sn, double* cs) {
     const double s = t * t;
-    double ps = kSinS[10], pc = kCosC[10];
+    coef_t* S = coef_at_use(kSinS);
+    coef_t* C = coef_at_use(kCosC);
+    double ps = S[10], pc = C[10];
 #pragma unroll
     for (int k = 9; k >= 0; --k) {
-        ps = fma(ps, s, kSinS[k]);
-        pc = fma(pc, s, kCosC[k]);
+        ps = fma_sc(ps, s, S[k]);
+        pc = fma_sc(pc, s, C[k]);
     }
     *sn = t * ps;
     *cs = pc;

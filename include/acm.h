@@ -539,12 +539,17 @@ ACM_API int acm_stream_synchronize(void *stream);
  * slower than the host loop (1.41 vs 1.33 ms at config 3) and never was the
  * default.  acm_set_tuning returns ACM_ERR_NOT_SUPPORTED; acm_lm_optimize
  * always runs the host loop.
+ * ACM_TUNE_ROUND_TRIP (r05): acm_project_unproject's pixels per lane and
+ * AoS ray stores: -1 = auto (the per-model default); else PPT (1, 2 or 4)
+ * + 8 x stores (0 = the model's default, 1 = each wave's 64 rays staged in
+ * LDS and written as 16-B pieces, 2 = three 8-B stores per ray).  Same
+ * outputs for every value.
  * Defaults (the value acm_set_tuning returns as "previous" in a fresh
  * process; tests/test_capi.py checks every one): PROJECT_VARIANT -1,
  * RESIDUAL_NT 0, NE_WAVES 0, FOV_UNROLL -1, NE_UNROLL 0, ALIGN_J -1,
  * NT_LOADS -1, NT_LOADS_UNPROJECT -1, LM_HOST_RESULT -1, SAMPLE_FUSED -1,
  * UNPROJECT_RCP -1, SAMPLE_PATIENCE -1, UNPROJECT_PPT -1, SAMPLE_CERT -1,
- * SAMPLE_WRITE -1.
+ * SAMPLE_WRITE -1, ROUND_TRIP -1.
  * Every knob is an atomic: acm_set_tuning may race with any other call.
  * Returns the previous value or an error. */
 enum {
@@ -564,7 +569,8 @@ enum {
     ACM_TUNE_UNPROJECT_PPT = 13,
     ACM_TUNE_SAMPLE_CERT = 14,
     ACM_TUNE_SAMPLE_WRITE = 15,
-    ACM_TUNE_LM_DEVICE = 16
+    ACM_TUNE_LM_DEVICE = 16,
+    ACM_TUNE_ROUND_TRIP = 17
 };
 ACM_API int acm_set_tuning(int key, int value);
 

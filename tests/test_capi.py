@@ -163,7 +163,8 @@ def test_tuning_knobs_validate_and_restore():
              _lib.TUNE_UNPROJECT_RCP: ([-1, 0, 1], [2, -2]),
              _lib.TUNE_SAMPLE_CERT: ([-1, 0], [1, -2]),
              _lib.TUNE_SAMPLE_WRITE: ([-1, 1, 2, 3, 4, 5], [6, -2]),
-             _lib.TUNE_UNPROJECT_PPT: ([-1, 1, 2, 3], [0, 4, -2])}
+             _lib.TUNE_UNPROJECT_PPT: ([-1, 1, 2, 3], [0, 4, -2]),
+             _lib.TUNE_ROUND_TRIP: ([-1, 1, 2, 4, 9, 10, 12, 17, 18, 20], [0, 3, 8, 21, -2])}
     for key, (good, bad) in cases.items():
         first = L.acm_set_tuning(key, good[0])
         assert first >= -1, key

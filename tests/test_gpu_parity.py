@@ -889,3 +889,38 @@ def test_project_unproject_fused_vs_oracle_golden(be, golden_dir, model, layout)
     assert np.array_equal(st, g["proj_status"])
     assert rel_err(uv, g["uv"], floor=1.0) <= TOL
     check_round_trip_vs_oracle(model, params, w, h, g["xyz"], uv, st, rays, st2)
+
+
+@pytest.mark.parametrize("model", range(7))
+def test_project_unproject_layout_knob_same_bits(model):
+    """ACM_TUNE_ROUND_TRIP (points per lane 1 / 2 / 4, LDS-staged or direct
+    AoS ray stores) selects among kernels with identical outputs: every
+    setting writes the default's pixels, statuses and rays bit for bit,
+    on a ragged size with the synthetic cloud's edge points."""
+    import ctypes
+    import torch
+    from apex_camera_models import _lib, samples
+    L = _lib.load()
+    params, (w, h) = samples.SAMPLES[model]
+    cam = _model_obj(model, params, w, h).acm_camera()
+    n = 300_001
+    pts = samples.synthetic_points_device(n)
+    sh = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        out = (torch.empty((n, 2), dtype=torch.float64, device="cuda"),
+               torch.empty((n,), dtype=torch.uint8, device="cuda"),
+               torch.empty((n, 3), dtype=torch.float64, device="cuda"),
+               torch.empty((n,), dtype=torch.uint8, device="cuda"))
+        _lib.check(L.acm_project_unproject(ctypes.byref(cam), n, pts.data_ptr(), 0,
+                                           out[0].data_ptr(), out[1].data_ptr(),
+                                           out[2].data_ptr(), out[3].data_ptr(), sh))
+        torch.cuda.synchronize()
+        return [t.cpu().numpy().tobytes() for t in out]
+    ref = run()
+    try:
+        for v in (1, 2, 4, 9, 10, 12, 17, 18, 20):
+            L.acm_set_tuning(_lib.TUNE_ROUND_TRIP, v)
+            assert run() == ref, v
+    finally:
+        L.acm_set_tuning(_lib.TUNE_ROUND_TRIP, -1)

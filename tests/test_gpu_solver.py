@@ -500,6 +500,23 @@ def test_initial_error_and_linear_estimation_errors():
     with pytest.raises(InvalidParams):
         util.initial_error_and_linear_estimation(m, torch.as_tensor(xyz[:3]),
                                                  torch.as_tensor(uv[:3]))
+    # a count mismatch is linear_estimation's InvalidParams
+    with pytest.raises(InvalidParams, match="must match"):
+        util.initial_error_and_linear_estimation(m, torch.as_tensor(xyz[:10]),
+                                                 torch.as_tensor(uv[:9]))
+    # an early error return of the C call (invalid camera) raises its own
+    # error, never a spurious ZeroProjectionPoints read off an unwritten result
+    bad = _model(KB, sp[:4] + [0.0] * 4, w, h)
+    good_cam = type(bad).acm_camera
+
+    def wrong_count():  # a camera struct whose num_params disagrees (check_cam)
+        c = good_cam(bad)
+        c.num_params = 3
+        return c
+    bad.acm_camera = wrong_count
+    with pytest.raises(InvalidParams, match="num_params"):
+        util.initial_error_and_linear_estimation(bad, torch.as_tensor(xyz[:100]),
+                                                 torch.as_tensor(uv[:100]))
 
 
 def _capi_reprojection(L, cam, p3, p2, layout, n):
