@@ -3507,6 +3507,101 @@ static unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 // range div_by_f is exact in) and the model's uniform subexpressions.
 // reference_newton (ACM_REFERENCE_NEWTON, per call): the reference's own
 // Newton loops for every pixel (KB, RadTan) and FOV's IEEE unprojection.
+// RadTan::newton_fast's certified disk (r05): the largest S (from a fixed
+// schedule, S <= 4) such that for every (x, y) with x^2 + y^2 <= S (1 + 1e-6)
+// the distortion Jacobian (rad_tan.rs:470-491) has det >= 1/16 (1 + 1e-6)
+// and |j00| + |j11| + 2 |j01| <= 64 (1 - 1e-6) -- the two conditions the fast
+// loop's error analysis needs, checked per step until r05 -- and |x|, |y| <=
+// 2 (implied by S <= 4).  Then one test of the iterate's own s = x^2 + y^2
+// replaces the per-step |x|, |y|, det and row-sum tests (~6 of the step's 77
+// VALU instructions).  Rigorous: the square around the disk is cut into
+// 128 x 128 cells and on every cell that meets the disk the Jacobian's
+// entries are enclosed by interval arithmetic (each bound widened by 4 ulp
+// of its magnitude, which covers the rounding of the host's own evaluation):
+//   rad = 1 + k1 s + k2 s^2 + k3 s^3, w = 2 (k1 + 2 k2 s + 3 k3 s^2),
+//   j00 = rad + x^2 w + 2 p1 y + 6 p2 x, j11 = rad + y^2 w + 6 p1 y + 2 p2 x,
+//   j01 = xy w + 2 p1 x + 2 p2 y (= j10), det = j00 j11 - j01^2.
+// 0 when no S qualifies: the loop keeps the per-step tests.  Memoised per
+// distortion vector (~1 ms of host time per schedule step).
+namespace hiv {  // host intervals (radtan_disk_ok)
+struct Iv {
+    double lo, hi;
+};
+inline Iv iv_w(double lo, double hi) {  // widen by 4 ulp of the magnitude
+    const double e = 4 * 0x1p-52;
+    return {lo - e * std::fabs(lo) - 1e-300, hi + e * std::fabs(hi) + 1e-300};
+}
+inline Iv operator+(Iv a, Iv b) { return iv_w(a.lo + b.lo, a.hi + b.hi); }
+inline Iv operator-(Iv a, Iv b) { return iv_w(a.lo - b.hi, a.hi - b.lo); }
+inline Iv operator*(Iv a, Iv b) {
+    const double p[4] = {a.lo * b.lo, a.lo * b.hi, a.hi * b.lo, a.hi * b.hi};
+    return iv_w(std::fmin(std::fmin(p[0], p[1]), std::fmin(p[2], p[3])),
+                std::fmax(std::fmax(p[0], p[1]), std::fmax(p[2], p[3])));
+}
+inline Iv operator*(double c, Iv a) { return Iv{c, c} * a; }
+inline Iv iv_sq(Iv a) {
+    const double l = std::fabs(a.lo), h = std::fabs(a.hi);
+    const double mx = std::fmax(l, h) * std::fmax(l, h);
+    const double mn = (a.lo <= 0.0 && a.hi >= 0.0) ? 0.0 : std::fmin(l, h) * std::fmin(l, h);
+    return iv_w(mn, mx);
+}
+inline double iv_mag(Iv a) { return std::fmax(std::fabs(a.lo), std::fabs(a.hi)); }
+}  // namespace hiv
+
+static bool radtan_disk_ok(const double* p, double S) {
+    using hiv::Iv;
+    using hiv::iv_sq;
+    using hiv::iv_mag;
+    const double k1 = p[4], k2 = p[5], p1 = p[6], p2 = p[7], k3 = p[8];
+    const double r = std::sqrt(S * (1.0 + 1e-6)) * (1.0 + 1e-12);
+    constexpr int G = 128;
+    const double h = 2.0 * r / G;
+    for (int i = 0; i < G; ++i) {
+        const Iv X{-r + h * i, -r + h * (i + 1)};
+        const double dx = X.lo > 0 ? X.lo : (X.hi < 0 ? -X.hi : 0.0);
+        for (int j = 0; j < G; ++j) {
+            const Iv Y{-r + h * j, -r + h * (j + 1)};
+            const double dy = Y.lo > 0 ? Y.lo : (Y.hi < 0 ? -Y.hi : 0.0);
+            if (dx * dx + dy * dy > r * r) continue;  // the cell misses the disk
+            const Iv X2 = iv_sq(X), Y2 = iv_sq(Y), XY = X * Y;
+            const Iv s = X2 + Y2, s2 = iv_sq(s);
+            const Iv rad = Iv{1, 1} + k1 * s + k2 * s2 + k3 * (s * s2);
+            const Iv w = 2.0 * (Iv{k1, k1} + (2 * k2) * s + (3 * k3) * s2);
+            const Iv j00 = rad + X2 * w + (2 * p1) * Y + (6 * p2) * X;
+            const Iv j11 = rad + Y2 * w + (6 * p1) * Y + (2 * p2) * X;
+            const Iv j01 = XY * w + (2 * p1) * X + (2 * p2) * Y;
+            const Iv det = j00 * j11 - iv_sq(j01);
+            const double sj = iv_mag(j00) + iv_mag(j11) + 2 * iv_mag(j01);
+            if (!(det.lo >= 0.0625 * (1.0 + 1e-6)) || !(sj <= 64.0 * (1.0 - 1e-6))) return false;
+        }
+    }
+    return true;
+}
+
+static double radtan_newton_disk_uncached(const double* p) {
+    for (int i = 4; i < 9; ++i)
+        if (!std::isfinite(p[i])) return 0.0;
+    for (double S : {4.0, 3.0, 2.5, 2.0, 1.6, 1.3, 1.0, 0.8, 0.6, 0.4, 0.25})
+        if (radtan_disk_ok(p, S)) return S;
+    return 0.0;
+}
+
+static double radtan_newton_disk(const double* p) {
+    static std::mutex mu;
+    static std::map<std::array<double, 5>, double> memo;
+    const std::array<double, 5> key{p[4], p[5], p[6], p[7], p[8]};
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = memo.find(key);
+        if (it != memo.end()) return it->second;
+    }
+    const double S = radtan_newton_disk_uncached(p);
+    std::lock_guard<std::mutex> lock(mu);
+    if (memo.size() > 256) memo.clear();
+    memo[key] = S;
+    return S;
+}
+
 static CamArg prep(acm_camera c, bool reference_newton = false) {
     if (c.model == ACM_FOV) c.params[8] = std::tan(c.params[4] / 2.0);
     CamArg a;
@@ -3519,6 +3614,9 @@ static CamArg prep(acm_camera c, bool reference_newton = false) {
     a.ifx = rcp ? recip(c.params[0]) : 0.0;
     a.ify = rcp ? recip(c.params[1]) : 0.0;
     unproject_consts<double>(c.model, c.params, a.uk);
+#ifndef ACM_AB_NO_RADTAN_DISK  // A/B build: the per-step tests of r04
+    if (c.model == ACM_RADTAN) a.uk[1] = radtan_newton_disk(c.params);
+#endif
     if (reference_newton &&
         (c.model == ACM_KANNALA_BRANDT || c.model == ACM_RADTAN || c.model == ACM_FOV))
         a.uk[0] = NAN;  // fast Newton loops / FOV fast unprojection off
@@ -4574,6 +4672,18 @@ ACM_API int acm_sample_points_certificate(const acm_camera* cam, double* out) {
     out[2] = c.all_hi;
     out[3] = c.none_lo;
     out[4] = c.none_hi;
+    return ACM_SUCCESS;
+}
+
+ACM_API int acm_unproject_certificate(const acm_camera* cam, double* out) {
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if (!out) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    out[0] = out[1] = 0.0;
+    if (cam->model != ACM_RADTAN) return ACM_SUCCESS;
+    const CamArg a = prep(*cam);
+    out[0] = a.uk[1];
+    out[1] = a.uk[0] == a.uk[0] ? 1.0 : 0.0;
     return ACM_SUCCESS;
 }
 

@@ -522,13 +522,62 @@ struct RadTan {
     // the caller runs newton_step from the start.
     __device__ static __forceinline__ bool newton_fast(const Cam<T>& c, T tx, T ty, T& px,
                                                        T& py) {
-        const T k1 = c.p[4], k2 = c.p[5], p1 = c.p[6], p2 = c.p[7], k3 = c.p[8];
+        const T k1 = c.p[4], k2 = c.p[5], p1 = c.p[6], p2 = c.p[7];
+        T k3 = c.p[8];
         const T k2d = k2 + k2, k3t = T(3) * k3, p1d = p1 + p1, p2d = p2 + p2;
         const T p1s = T(6) * p1, p2s = T(6) * p2;
         constexpr T lo = T(kNewtonTol2) * (T(1) - T(0x1p-10));
         constexpr T hi = T(kNewtonTol2) * (T(1) + T(0x1p-10));
         T x = tx, y = ty;
         int state = 0;  // 0 iterating, 1 certified converged, 2 uncertain
+        // uk[1] = S > 0 (r05, acm.hip radtan_newton_disk): on the disk
+        // x^2 + y^2 <= S the host has bounded |det| >= 1/16 and the row sums
+        // <= 64 for every point, so the step needs only the test s <= S.  k3
+        // is copied to a VGPR once: fma(k3, s, k2) with both in SGPRs cost a
+        // v_mov per step (one scalar operand per VALU instruction).
+        const T S = c.uk[1];
+        if (S > T(0)) {
+            asm volatile("" : "+v"(k3));
+#pragma unroll 1
+            for (int i = 0; i < 12 && state == 0; ++i) {
+                const T x2 = x * x, y2 = y * y, xy = x * y;
+                const T s = x2 + y2;
+                int st;
+                if (!(s <= S)) {
+                    st = 2;  // outside the disk, or NaN
+                } else {
+                    const T rad = fma(fma(fma(k3, s, k2), s, k1), s, T(1));
+                    const T xe = fma(x, rad, fma(p1d, xy, p2 * fma(x + x, x, s)));
+                    const T ye = fma(y, rad, fma(p1, fma(y + y, y, s), p2d * xy));
+                    const T ex = xe - tx, ey = ye - ty;
+                    const T en2 = fma(ex, ex, ey * ey);
+                    if (en2 < lo) {
+                        st = 1;  // :459 breaks before the step
+                    } else if (!(en2 > hi)) {
+                        st = 2;  // in the band, or NaN
+                    } else {
+                        const T cm = fma(fma(k3t, s, k2d), s, k1);
+                        const T w = cm + cm;
+                        const T j00 = fma(x2, w, rad) + fma(p1d, y, p2s * x);
+                        const T j11 = fma(y2, w, rad) + fma(p1s, y, p2d * x);
+                        const T j01 = fma(xy, w, fma(p1d, x, p2d * y));
+                        const T det = fma(j00, j11, -(j01 * j01));
+                        const T r0 = __builtin_amdgcn_rcp(det);
+                        const T id = fma(r0, fma(-det, r0, T(1)), r0);
+                        const T dx = fma(j11, ex, -(j01 * ey)) * id;
+                        const T dy = fma(j00, ey, -(j01 * ex)) * id;
+                        x -= dx;
+                        y -= dy;
+                        const T dn2 = fma(dx, dx, dy * dy);
+                        st = dn2 < lo ? 1 : (dn2 > hi ? 0 : 2);  // :503
+                    }
+                }
+                state = st;
+            }
+            px = x;
+            py = y;
+            return state == 1;
+        }
 #pragma unroll 1
         for (int i = 0; i < 12 && state == 0; ++i) {
             const T x2 = x * x, y2 = y * y, xy = x * y;

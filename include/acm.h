@@ -426,6 +426,14 @@ ACM_API int acm_sample_points_range(const acm_camera *cam, size_t n_requested,
  * [none_lo, none_hi]; on = 0: no certificate (every segment is counted cell
  * by cell).  Host only. */
 ACM_API int acm_sample_points_certificate(const acm_camera *cam, double *out);
+/* (r05) RadTan only: the host-certified disk of acm_unproject's fast Newton
+ * loop (csrc/acm.hip radtan_newton_disk).  out = [S, fast]: for every (x, y)
+ * with x^2 + y^2 <= S the distortion Jacobian has |det| >= 1/16 and
+ * |j00| + |j11| + 2 |j01| <= 64, so the loop tests only s <= S per step
+ * (S = 0: no disk, the per-step tests); fast = 1 when the certified fast
+ * loop runs at all (its distortion bound holds).  Host only; [0, 0] for the
+ * other models. */
+ACM_API int acm_unproject_certificate(const acm_camera *cam, double *out);
 /* (r04) KB only: how acm_sample_points forms the rays of cells inside the
  * certified kept interval.  out = [mode, M, ef, fit_err, all_lo, all_hi]:
  * mode 0 = the reference-iterate path for every cell, 1 / 2 = the root by
