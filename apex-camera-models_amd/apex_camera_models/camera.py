@@ -239,18 +239,23 @@ class CameraModel:
                       jac.data_ptr() if jac is not None else None, _stream_handle()))
         return uv, st, jac
 
-    def unproject_batch(self, points_2d, layout: str = "aos", reference_newton: bool = False):
+    def unproject_batch(self, points_2d, layout: str = "aos", reference_newton: bool = False,
+                        out: Optional[Tuple[Optional[torch.Tensor], ...]] = None):
         """Batched `CameraModel::unproject` (mod.rs:271).  Returns (rays, status).
         reference_newton=True: ACM_REFERENCE_NEWTON for this call (the
-        reference's own Newton loops; include/acm.h)."""
+        reference's own Newton loops; include/acm.h).  out = (rays, status):
+        preallocated outputs (either may be None)."""
         uv = _as_device_f64(points_2d, 2)
         n = uv.shape[0]
         lay = _lib.LAYOUT_SOA if layout == "soa" else _lib.LAYOUT_AOS
         if reference_newton:
             lay |= _lib.REFERENCE_NEWTON
-        rays = torch.empty((n, 3) if layout != "soa" else (3, n), dtype=torch.float64,
-                           device=uv.device)
-        st = torch.empty((n,), dtype=torch.uint8, device=uv.device)
+        rays, st = out if out is not None else (None, None)
+        if rays is None:
+            rays = torch.empty((n, 3) if layout != "soa" else (3, n), dtype=torch.float64,
+                               device=uv.device)
+        if st is None:
+            st = torch.empty((n,), dtype=torch.uint8, device=uv.device)
         cam = self.acm_camera()
         _lib.check(_lib.load().acm_unproject(ctypes.byref(cam), n, uv.data_ptr(),
                                               rays.data_ptr(), lay, st.data_ptr(),

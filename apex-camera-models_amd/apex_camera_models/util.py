@@ -208,6 +208,26 @@ class ValidationResults:
 
 _REGIONS = (("Center", 0.5), ("Near Center", 0.55), ("Mid Region", 0.65),
             ("Edge Region", 0.8), ("Far Edge", 0.95))
+_VALIDATION_CACHE = {}
+
+
+def _validation_buffers(width: int, height: int):
+    """The five test pixels of a resolution, resident on the device, and the
+    device / pinned-host result buffers of validate_conversion_accuracy
+    (cached per resolution and device: the call then launches three kernels
+    and copies twice, without building tensors on the host)."""
+    key = (int(width), int(height), torch.cuda.current_device())
+    if key not in _VALIDATION_CACHE:
+        w, h = float(width), float(height)
+        k = len(_REGIONS)
+        pix = torch.tensor([[w * f, h * f] for _, f in _REGIONS], dtype=torch.float64,
+                           device="cuda")
+        _VALIDATION_CACHE[key] = (
+            pix, torch.empty((3 * k,), dtype=torch.uint8, device="cuda"),
+            torch.empty((2 * k, 2), dtype=torch.float64, device="cuda"),
+            torch.empty((3 * k,), dtype=torch.uint8).pin_memory(),
+            torch.empty((2 * k, 2), dtype=torch.float64).pin_memory())
+    return _VALIDATION_CACHE[key]
 
 
 def validate_conversion_accuracy(output_model: CameraModel,
@@ -218,19 +238,19 @@ def validate_conversion_accuracy(output_model: CameraModel,
     (one batched kernel call each); error = ||input_proj - output_proj||."""
     import math
     res = input_model.get_resolution()
-    w, h = float(res.width), float(res.height)
-    pix = torch.tensor([[w * f, h * f] for _, f in _REGIONS], dtype=torch.float64)
-    rays, st_u = input_model.unproject_batch(pix)
-    uv_in, st_in, _ = input_model.project_batch(rays)
-    uv_out, st_out, _ = output_model.project_batch(rays)
-    # one device -> host read for all five outputs (each .cpu() is a sync)
     k = len(_REGIONS)
-    flat = torch.cat([st_u.reshape(-1).to(torch.float64), st_in.reshape(-1).to(torch.float64),
-                      st_out.reshape(-1).to(torch.float64), uv_in.reshape(-1),
-                      uv_out.reshape(-1)]).cpu().tolist()
-    rays_ok, ok_in, ok_out = flat[:k], flat[k:2 * k], flat[2 * k:3 * k]
-    a = [flat[3 * k + 2 * j: 3 * k + 2 * j + 2] for j in range(k)]
-    b = [flat[5 * k + 2 * j: 5 * k + 2 * j + 2] for j in range(k)]
+    pix, st_d, uv_d, st_h, uv_h = _validation_buffers(res.width, res.height)
+    rays, _ = input_model.unproject_batch(pix, out=(None, st_d[:k]))
+    input_model.project_batch(rays, out=(uv_d[:k], st_d[k:2 * k], None))
+    output_model.project_batch(rays, out=(uv_d[k:], st_d[2 * k:], None))
+    # two async copies into pinned host memory and one stream synchronisation
+    st_h.copy_(st_d, non_blocking=True)
+    uv_h.copy_(uv_d, non_blocking=True)
+    torch.cuda.current_stream().synchronize()
+    st = st_h.tolist()
+    uvl = uv_h.tolist()
+    rays_ok, ok_in, ok_out = st[:k], st[k:2 * k], st[2 * k:]
+    a, b = uvl[:k], uvl[k:]
     total, max_error, valid = 0.0, 0.0, 0
     errs, data = [], []
     for i, (name, _) in enumerate(_REGIONS):

@@ -125,15 +125,23 @@ __constant__ double kAtanO[10] = {  // odd-index coefficients c1, c3, ..., c19
 // the two-operand v_fmac_f64 and first copied every coefficient into a VGPR
 // pair (two v_mov_b32 per Horner step).  The same single rounding as fma().
 typedef __attribute__((address_space(4))) const double coef_t;
+// (Unoptimised device builds -- the host-sanitizer tests compile the device
+// side at -O0 -- cannot place these operands in SGPRs: plain forms there.)
 __device__ __forceinline__ coef_t* coef_at_use(const double* table) {
     coef_t* p = (coef_t*)table;
+#ifdef __OPTIMIZE__
     asm volatile("" : "+s"(p));
+#endif
     return p;
 }
 __device__ __forceinline__ double fma_sc(double a, double b, double c) {
+#ifdef __OPTIMIZE__
     double r;
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
     return r;
+#else
+    return fma(a, b, c);
+#endif
 }
 
 __device__ __forceinline__ double atan01(double b) {

@@ -36,14 +36,18 @@ def main():
     cold, _ = wall(lambda: conversion.convert(src, "double_sphere", xyz, uv))
     warm = [wall(lambda: conversion.convert(src, "double_sphere", xyz, uv))[0]
             for _ in range(a.reps)]
-    stages = {k: [] for k in ("init_target", "initial_reproj", "linear_estimation", "lm",
-                              "final_reproj", "validation")}
+    stages = {k: [] for k in ("init_target", "initial_reproj", "linear_estimation",
+                              "initial_and_linear_fused", "lm", "final_reproj", "validation")}
     for _ in range(a.reps):
         t, m = wall(lambda: conversion._init_target("double_sphere", src))
         stages["init_target"].append(t)
         stages["initial_reproj"].append(wall(lambda: util.compute_reprojection_error(
             m, xyz, uv))[0])
         stages["linear_estimation"].append(wall(lambda: m.linear_estimation(xyz, uv))[0])
+        # what convert() runs (r04): the two stages above in one pass
+        m2 = conversion._init_target("double_sphere", src)
+        stages["initial_and_linear_fused"].append(wall(
+            lambda: util.initial_error_and_linear_estimation(m2, xyz, uv))[0])
         t, res = wall(lambda: LevenbergMarquardt().optimize(
             m, xyz, uv, bounds=CONVERTER_BOUNDS["double_sphere"]))
         stages["lm"].append(t)
