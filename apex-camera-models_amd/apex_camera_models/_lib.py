@@ -136,6 +136,7 @@ EXPORTED_SYMBOLS = (
     "acm_sample_points_ex",
     "acm_sample_points_certificate",
     "acm_unproject_certificate",
+    "acm_sample_points_ray_poly",
     "acm_sample_points_ray_fit",
     "acm_undistort_image",
     "acm_set_device",
@@ -232,6 +233,8 @@ def load():
     L.acm_sample_points_certificate.restype = i
     L.acm_unproject_certificate.argtypes = [cam_p, ctypes.POINTER(ctypes.c_double)]
     L.acm_unproject_certificate.restype = i
+    L.acm_sample_points_ray_poly.argtypes = [cam_p, ctypes.POINTER(ctypes.c_double)]
+    L.acm_sample_points_ray_poly.restype = i
     L.acm_sample_points_ray_fit.argtypes = [cam_p, ctypes.POINTER(ctypes.c_double)]
     L.acm_sample_points_ray_fit.restype = i
     L.acm_linear_system_columns.argtypes = [i]

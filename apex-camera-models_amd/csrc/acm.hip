@@ -1783,8 +1783,9 @@ struct SegCert {
     double rp[2 * kRayPolyN];  // KB: cos theta*, sin theta* / ru ~= sum rp[i] r2^i, sum rp[N + i] r2^i
     // KB: M = cmax / (2 dmin) of the Newton analysis, ef = the bound on
     // |theta_ref - theta*| (the reference's final iterate vs the root, which
-    // the certified rays use), and the ray polynomials' sampled fit error
-    double M, ef, rp_err;
+    // the certified rays use), and the bound on the ray polynomials' error
+    // (kb_ray_poly_bound)
+    double M, ef, rp_err, ig_err;  // ig_err: the bound on the initial guess (kb_guess_bound)
 };
 
 // Rigorous bounds of r2 = mx^2 + my^2 over the cells [c0, c1] (inclusive,
@@ -3727,14 +3728,15 @@ static SegCert kb_seg_cert_on(const double* p, double tmax) {
 // not below pi/2); the certificate covering the most is kept.
 // KB: theta*(ru) ~= ru g(ru^2), g the degree-8 interpolant of theta*(ru)/ru
 // in s = ru^2 at Chebyshev nodes on [0, all_hi^2] (theta* solved in long
-// double).  Over 4001 points of the interval its error e0 decides
-// ray_certified's Newton steps: one when M e0^2 <= 1e-17 (M as in
-// kb_seg_cert_on), two when M^3 e0^4 <= 1e-13 and e0 <= 1e-5, else the fit
-// is not used (ig_ok = 0).  The error is SAMPLED (4001 points), not bounded.
+// double).  Its error e0 over the whole interval (kb_guess_bound, r05: a
+// bound; r04 sampled 4001 points) decides ray_certified's Newton steps: one
+// when M e0^2 <= 1e-17 (M as in kb_seg_cert_on), two when M^3 e0^4 <= 1e-13
+// and e0 <= 1e-5, else the fit is not used (ig_ok = 0).
 // Certified rays are the root's, the reference returns its last iterate:
 // they differ by up to ef = M (1.01e-6)^2 + 2 eta (kb_seg_cert_on), so the
 // rays are used only while ef <= 1e-11, a tenth of the 1e-10 bar (ADVICE
 // r03); otherwise every cell takes the reference-iterate path.
+static double kb_guess_bound(const double* p, const double* ig, long double Th);
 static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
     s.ig_ok = 0;
     const long double k1 = p[4], k2 = p[5], k3 = p[6], k4 = p[7];
@@ -3776,15 +3778,161 @@ static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
         }
     }
     for (int i = 0; i < N; ++i) s.ig[i] = (double)(A[i][N] / A[i][i]);
-    double e0 = 0.0;
-    for (int i = 0; i <= 4000; ++i) {
-        const double ru = R * i / 4000.0;
-        double g = s.ig[N - 1];
-        for (int k = N - 2; k >= 0; --k) g = std::fma(g, ru * ru, s.ig[k]);
-        e0 = std::fmax(e0, std::fabs((double)((long double)ru * g - root(ru))));
-    }
+    // a bound over the interval (r05; r04 sampled 4001 points)
+    const double e0 = kb_guess_bound(p, s.ig, root((long double)R) * (1 + 1e-12L));
+    s.ig_err = e0;
     s.ig_ok = M * e0 * e0 <= 1e-17 ? 1 : (e0 <= 1e-5 && M * M * M * e0 * e0 * e0 * e0 <= 1e-13 ? 2 : 0);
     if (!(s.ef <= 1e-11)) s.ig_ok = 0;
+}
+
+// A bound on the ray polynomials' error (r05; replaces
+// a check on 16385 sample points).  The cells use the polynomials for s =
+// r2 in [0, Sm], Sm = all_hi^2, i.e. for theta = theta*(sqrt(s)) in [0, Th],
+// Th = theta*(all_hi).  In theta the errors are explicit functions, with no
+// root to solve:
+//   F1(theta) = C(s(theta)) - cos(theta),
+//   F2(theta) = theta_d(theta) S(s(theta)) - sin(theta)   (= ru (S - S*)),
+// s(theta) = theta_d(theta)^2, theta_d(theta) = theta (1 + k1 theta^2 + ...
+// + k4 theta^8), C and S the fitted polynomials with their double
+// coefficients.  [0, Th] is cut into kRayBoundCells pieces [m - r, m + r];
+// on each, Taylor's theorem gives
+//   |F(m + t)| <= sum_{k < J} |F_k| r^k + B_J r^J,
+// F_k the Taylor coefficients at m, computed exactly up to rounding by
+// truncated power-series (jet) arithmetic in long double, and B_J a bound on
+// the J-th Taylor coefficient anywhere on the piece: the J-th coefficient of
+// the majorant -- the same composition with every coefficient (p_i, k_i)
+// replaced by its absolute value, taken at a = m + r -- plus 1 / J! for
+// cos / sin.  (A polynomial in theta whose coefficients dominate another's
+// in absolute value dominates every Taylor coefficient of it at any |xi| <=
+// a; sums, products and compositions of such majorants are majorants.)  The
+// jets' own rounding is covered by 2^-53 times the majorant's coefficient
+// (>= 1000 long-double operations' worth of 2^-64 each).  To that the bound
+// adds the device's evaluation error: Horner with FMAs in double over
+// kRayPolyN terms, gamma_N |P|(Sm), plus one rounding of X = mx S.
+namespace {
+constexpr int kRayBoundCells = 256;
+constexpr int kRayJ = 8;  // Taylor order of the remainder term
+struct Jet {
+    long double c[kRayJ + 1];
+};
+Jet jet_const(long double v) {
+    Jet r{};
+    r.c[0] = v;
+    return r;
+}
+Jet jet_mul(const Jet& a, const Jet& b) {
+    Jet r{};
+    for (int i = 0; i <= kRayJ; ++i)
+        for (int j = 0; i + j <= kRayJ; ++j) r.c[i + j] += a.c[i] * b.c[j];
+    return r;
+}
+Jet jet_fma(const Jet& a, const Jet& b, long double c0) {  // a * b + c0
+    Jet r = jet_mul(a, b);
+    r.c[0] += c0;
+    return r;
+}
+// theta_d and s = theta_d^2 as jets of theta = x + t (ABS: |k_i|, the majorant)
+void jet_thd_s(const double* p, long double x, bool abs_, Jet& thd, Jet& s) {
+    Jet th = jet_const(x);
+    th.c[1] = 1;
+    const Jet t2 = jet_mul(th, th);
+    auto k = [&](int i) { return abs_ ? std::fabs((long double)p[i]) : (long double)p[i]; };
+    Jet q = jet_const(k(7));
+    q = jet_fma(q, t2, k(6));
+    q = jet_fma(q, t2, k(5));
+    q = jet_fma(q, t2, k(4));
+    q = jet_fma(q, t2, 1.0L);
+    thd = jet_mul(th, q);
+    s = jet_mul(thd, thd);
+}
+Jet jet_poly(const double* c, const Jet& s, bool abs_, int n = kRayPolyN) {  // sum c_i s^i
+    auto k = [&](int i) { return abs_ ? std::fabs((long double)c[i]) : (long double)c[i]; };
+    Jet r = jet_const(k(n - 1));
+    for (int i = n - 2; i >= 0; --i) r = jet_fma(r, s, k(i));
+    return r;
+}
+}  // namespace
+
+// The same bound for kb_fit_initial_guess's theta_0 = ru g(ru^2) (modes 1 /
+// 2): F(theta) = theta_d(theta) g(s(theta)) - theta on [0, Th] (the initial
+// error e0 against the root the Newton steps solve for), plus the device's
+// evaluation of it (ru from rsq, s0 = RN(ru^2), Horner with FMAs over the 9
+// coefficients, one rounding of ru g).
+static double kb_guess_bound(const double* p, const double* ig, long double Th) {
+    constexpr int NG = 9;
+    const long double r = Th / (2 * kRayBoundCells);
+    long double worst = 0;
+    for (int cell = 0; cell < kRayBoundCells; ++cell) {
+        const long double m = (2 * cell + 1) * r;
+        Jet thd, s, thda, sa;
+        jet_thd_s(p, m, false, thd, s);
+        jet_thd_s(p, m + r, true, thda, sa);
+        const Jet G = jet_mul(thd, jet_poly(ig, s, false, NG));
+        const Jet Ga = jet_mul(thda, jet_poly(ig, sa, true, NG));
+        long double rk = 1, b = 0;
+        for (int k = 0; k < kRayJ; ++k) {
+            const long double id = k == 0 ? m : (k == 1 ? 1.0L : 0.0L);  // theta's coefficients
+            b += (std::fabs(G.c[k] - id) + 0x1p-53L * (Ga.c[k] + id)) * rk;
+            rk *= r;
+        }
+        b += Ga.c[kRayJ] * rk;
+        worst = std::fmax(worst, b);
+    }
+    Jet thd, s;
+    jet_thd_s(p, Th, true, thd, s);
+    const long double R = thd.c[0], Sm = s.c[0];
+    Jet sj = jet_const(Sm);
+    sj.c[1] = 1;
+    const Jet Gm = jet_poly(ig, sj, true, NG);  // |g|(Sm), |g|'(Sm)
+    const long double u = 0x1p-53L, gam = NG * u / (1 - NG * u);
+    const long double dev = R * (gam * Gm.c[0] + Gm.c[1] * 4 * u * Sm + 4 * u * Gm.c[0]) + 2 * u * Th;
+    return (double)(worst + dev) * (1 + 0x1p-40);
+}
+
+// max over [0, Th] of |F1| and |F2| (+ the device's evaluation error): a
+// bound, not a sample; rp: [C_0..C_{N-1} | S_0..S_{N-1}]
+static double kb_ray_poly_bound(const double* p, const double* rp, long double Th) {
+    constexpr int N = kRayPolyN;
+    long double jf = 1;  // J!
+    for (int k = 2; k <= kRayJ; ++k) jf *= k;
+    const long double r = Th / (2 * kRayBoundCells);
+    long double worst = 0;
+    for (int cell = 0; cell < kRayBoundCells; ++cell) {
+        const long double m = (2 * cell + 1) * r;
+        Jet thd, s;
+        jet_thd_s(p, m, false, thd, s);
+        const Jet Cj = jet_poly(rp, s, false);
+        const Jet Sj = jet_mul(thd, jet_poly(rp + N, s, false));
+        Jet thda, sa;
+        jet_thd_s(p, m + r, true, thda, sa);
+        const Jet Ca = jet_poly(rp, sa, true);
+        const Jet Sa = jet_mul(thda, jet_poly(rp + N, sa, true));
+        const long double cm = std::cos(m), sm = std::sin(m);
+        // Taylor coefficients of cos / sin at m: derivatives cycle
+        const long double dc[4] = {cm, -sm, -cm, sm}, ds[4] = {sm, cm, -sm, -cm};
+        long double kf = 1, rk = 1, b1 = 0, b2 = 0;
+        for (int k = 0; k < kRayJ; ++k) {
+            if (k > 1) kf *= k;
+            const long double f1 = Cj.c[k] - dc[k & 3] / kf;
+            const long double f2 = Sj.c[k] - ds[k & 3] / kf;
+            // rounding of the jets: 2^-53 of the majorant's coefficient
+            b1 += (std::fabs(f1) + 0x1p-53L * (Ca.c[k] + 1 / kf)) * rk;
+            b2 += (std::fabs(f2) + 0x1p-53L * (Sa.c[k] + 1 / kf)) * rk;
+            rk *= r;
+        }
+        b1 += (Ca.c[kRayJ] + 1 / jf) * rk;
+        b2 += (Sa.c[kRayJ] + 1 / jf) * rk;
+        worst = std::fmax(worst, std::fmax(b1, b2));
+    }
+    // the device: Horner with FMAs over N terms in double, gamma_N |P|(Sm);
+    // X = mx S rounds once more (|X| <= 1)
+    Jet thd, s;
+    jet_thd_s(p, Th, true, thd, s);
+    const long double PC = jet_poly(rp, s, true).c[0];
+    const long double PS = jet_mul(thd, jet_poly(rp + N, s, true)).c[0];
+    const long double u = 0x1p-53L, gam = N * u / (1 - N * u);
+    const long double dev = gam * std::fmax(PC, PS) + 2 * u;
+    return (double)(worst + dev) * (1 + 0x1p-40);
 }
 
 // KB's certified-cell rays as polynomials in s = ru^2 on [0, all_hi^2]:
@@ -3793,13 +3941,11 @@ static void kb_fit_initial_guess(const double* p, double M, SegCert& s) {
 // function of ru), so degree 16 interpolants at Chebyshev nodes, solved in
 // long double (backward-stable elimination: the computed polynomials match
 // the node values to ~1e-18, and the Chebyshev nodes keep them as close in
-// between), reach rounding level.  The fit is checked, not bounded: the
-// error against long-double roots on 16385 points of the interval (spacing
-// ~1.5e-4 of r2, against 16 node gaps) must be <= 1e-13, and with the
-// root-vs-reference distance ef, ef + error <= 1e-11 (the rays are held to
-// 1e-10), or rp_ok stays 0 and ray_certified keeps its Newton form (which the
-// ef gate of kb_fit_initial_guess covers in turn).  DESIGN.md §9 says
-// "sampled" for this check.
+// between), reach rounding level.  The error is BOUNDED (kb_ray_poly_bound,
+// r05): it must be <= 1e-13, and with the root-vs-reference distance ef, ef
+// + error <= 1e-11 (the rays are held to 1e-10), or rp_ok stays 0 and
+// ray_certified keeps its Newton form (which the ef gate of
+// kb_fit_initial_guess covers in turn).
 static void kb_fit_ray(const double* p, SegCert& s) {
     s.rp_ok = 0;
     const long double k1 = p[4], k2 = p[5], k3 = p[6], k4 = p[7];
@@ -3849,20 +3995,9 @@ static void kb_fit_ray(const double* p, SegCert& s) {
         }
         for (int i = 0; i < N; ++i) s.rp[which * N + i] = (double)(A[i][N] / A[i][i]);
     }
-    double err = 0.0;
-    constexpr int kChecks = 16384;
-    for (int i = 0; i <= kChecks; ++i) {
-        const double sv = (double)Sm * i / kChecks;
-        double C = s.rp[N - 1], S = s.rp[2 * N - 1];
-        for (int k = N - 2; k >= 0; --k) {
-            C = std::fma(C, sv, s.rp[k]);
-            S = std::fma(S, sv, s.rp[N + k]);
-        }
-        long double Ct, St;
-        cs(sv, Ct, St);
-        err = std::fmax(err, std::fabs((double)(C - Ct)));
-        err = std::fmax(err, std::fabs((double)(S - St)) * std::sqrt(sv));  // X = mx S, |m| = ru
-    }
+    // theta*(all_hi), rounded up: the bound covers every cell's theta*
+    const long double Th = root((long double)R) * (1 + 1e-12L);
+    const double err = kb_ray_poly_bound(p, s.rp, Th);
     s.rp_err = err;
     s.rp_ok = std::isfinite(err) && err <= 1e-13 && s.ef + err <= 1e-11;
 }
@@ -4701,6 +4836,24 @@ ACM_API int acm_sample_points_ray_fit(const acm_camera* cam, double* out) {
     out[3] = c.on ? c.rp_err : 0.0;
     out[4] = c.all_lo;
     out[5] = c.all_hi;
+    return ACM_SUCCESS;
+}
+
+ACM_API int acm_sample_points_ray_poly(const acm_camera* cam, double* out) {
+    static_assert(ACM_RAY_POLY_N == kRayPolyN, "acm.h ACM_RAY_POLY_N");
+    static_assert(ACM_RAY_GUESS_N == sizeof(SegCert::ig) / sizeof(double), "acm.h ACM_RAY_GUESS_N");
+    int rc = check_cam(cam);
+    if (rc) return rc;
+    if (!out) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    constexpr int NO = 2 * kRayPolyN + ACM_RAY_GUESS_N + 1;
+    for (int i = 0; i < NO; ++i) out[i] = 0.0;
+    if (cam->model != ACM_KANNALA_BRANDT) return ACM_SUCCESS;
+    const SegCert c = seg_cert(*cam);
+    if (c.on && c.all_hi > c.all_lo) {
+        for (int i = 0; i < 2 * kRayPolyN; ++i) out[i] = c.rp[i];
+        for (int i = 0; i < ACM_RAY_GUESS_N; ++i) out[2 * kRayPolyN + i] = c.ig[i];
+        out[NO - 1] = c.ig_err;
+    }
     return ACM_SUCCESS;
 }
 

@@ -890,7 +890,7 @@ struct KannalaBrandt {
     // read off two polynomials in r2 = ru^2 the host fits per camera on the
     // certified interval, C(r2) = cos(theta*(ru)) and S(r2) = sin(theta*(ru))
     // / ru (both analytic in r2; long-double roots at Chebyshev nodes, the
-    // error measured on 4001 points and required <= 1e-13, kb_fit_ray): X =
+    // error bounded and required <= 1e-13, kb_fit_ray): X =
     // mx S, Y = my S, Z = C -- 34 FMAs instead of the square root, the
     // initial guess, the Newton step and sin / cos (~55 FP64 operations).
     // POLY selects the form at compile time (the launcher picks the kernel

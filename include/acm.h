@@ -440,10 +440,22 @@ ACM_API int acm_unproject_certificate(const acm_camera *cam, double *out);
  * the fitted initial guess + 1 / 2 Newton steps, 3 = the ray polynomials;
  * M = the Newton error constant, ef = the bound on the distance between the
  * reference's final iterate and the root the certified rays use (modes 1-3
- * require ef <= 1e-11), fit_err = the ray polynomials' error, sampled on
- * 16385 points (mode 3 requires <= 1e-13).  Zeros for other models.  Host
- * only. */
+ * require ef <= 1e-11), fit_err = a bound on the ray polynomials' error
+ * over the whole certified interval, incl. the device's evaluation rounding
+ * (r05: Taylor remainders on 256 pieces, csrc/acm.hip kb_ray_poly_bound;
+ * r04 sampled it on 16385 points; mode 3 requires <= 1e-13).  Zeros for
+ * other models.  Host only. */
 ACM_API int acm_sample_points_ray_fit(const acm_camera *cam, double *out);
+/* (r05) KB only: the fitted polynomials themselves, for independent checks
+ * of the bounds.  out = 2 * ACM_RAY_POLY_N + ACM_RAY_GUESS_N + 1 doubles:
+ * [C_0 .. C_16 | S_0 .. S_16] (cos(theta*) and sin(theta*) / ru in powers of
+ * r2; what acm_sample_points evaluates when ray_fit's mode is 3), [g_0 ..
+ * g_8] (theta* / ru in powers of r2, the initial guess of modes 1 / 2) and
+ * the bound on |ru g(r2) - theta*| over the certified interval.  Zeros when
+ * no fit was made.  Host only. */
+#define ACM_RAY_POLY_N 17
+#define ACM_RAY_GUESS_N 9
+ACM_API int acm_sample_points_ray_poly(const acm_camera *cam, double *out);
 
 /* acm_sample_points_range with per-call options: flags = 0 or
  * ACM_REFERENCE_NEWTON.  (acm_sample_points / _range = flags 0.) */

@@ -2,7 +2,7 @@
 reference's own Newton loop per cell, point_sampling.rs:46-120 +
 kannala_brandt.rs:445-562), covering every way the kernels form the ray of a
 cell inside the host-certified kept interval (acm_sample_points_ray_fit):
-mode 3 (the ray polynomials) including draws whose sampled fit error lands
+mode 3 (the ray polynomials) including draws whose fit-error bound lands
 near the 1e-13 gate, mode 2 (fitted guess + two Newton steps), and cameras
 whose root-vs-iterate bound ef exceeds 1e-11, so the certified rays are off
 and every cell takes the reference-iterate path.  Kept sets and

@@ -103,7 +103,9 @@ def test_ray_fit_gates():
     """acm_sample_points_ray_fit (r04): the certified rays (the
     root theta*, not the reference's last iterate) are used only while the
     root-vs-iterate bound ef <= 1e-11, and the ray polynomials only while
-    their sampled error <= 1e-13; on the sample camera both hold."""
+    the bound on their error <= 1e-13 (r05: a bound, see
+    test_ray_poly_bound_holds; r04 sampled it); on the sample camera both
+    hold."""
     mode, M, ef, err, lo, hi = ray_fit(KB_SAMPLE)
     assert mode == 3 and ef <= 1e-11 and 0 < err <= 1e-13 and lo < hi
     rng = np.random.default_rng(11)
@@ -126,3 +128,58 @@ def test_ray_fit_gates():
     out = (ctypes.c_double * 6)()
     _lib.check(L.acm_sample_points_ray_fit(ctypes.byref(cam), out))
     assert list(out) == [0.0] * 6
+
+
+def ray_poly(params, w=512, h=512):
+    L = _lib.load()
+    cam = _lib.AcmCamera()
+    _lib.check(L.acm_camera_init(ctypes.byref(cam), 2, (ctypes.c_double * 8)(*params), 8, w, h))
+    out = (ctypes.c_double * 44)()
+    _lib.check(L.acm_sample_points_ray_poly(ctypes.byref(cam), out))
+    return list(out)
+
+
+def test_ray_poly_bound_holds():
+    """fit_err is a bound (r05, VERDICT r04 item 8: kb_ray_poly_bound, Taylor
+    remainders with majorant coefficients) on the ray polynomials' error over
+    the certified interval: re-derived here independently in 40-digit mpmath
+    -- theta* by root finding, the polynomials with their exact double
+    coefficients -- on 1500 points per camera (ends included), the error of
+    both cos(theta*) and ru (sin(theta*) / ru - S) never exceeds it, for the
+    sample camera and random ones; and it is not vacuous (<= 1e-13 on the
+    sample camera, which therefore uses the polynomials).  The same for the
+    initial guess of modes 1 / 2 (kb_guess_bound): |ru g(ru^2) - theta*| never
+    exceeds its bound."""
+    import mpmath as mp
+    mp.mp.dps = 40
+    rng = np.random.default_rng(5)
+    cams = [KB_SAMPLE] + [[200.0, 200.0, 256.0, 256.0] + list(rng.normal(0, sc * np.array(
+        [1.0, 0.5, 0.2, 0.05]))) for sc in (0.05, 0.2) for _ in range(8)]
+    checked = 0
+    for p in cams:
+        mode, M, ef, bound, lo, hi = ray_fit(p)
+        rp = ray_poly(p)
+        if not any(rp[:34]) or not np.isfinite(bound) or bound == 0.0:
+            continue
+        G = [mp.mpf(x) for x in rp[34:43]]
+        gbound = rp[43]
+        k = [mp.mpf(x) for x in p[4:]]
+        thd = lambda t: t * (1 + t**2 * (k[0] + t**2 * (k[1] + t**2 * (k[2] + t**2 * k[3]))))  # noqa: E731
+        th_max = mp.findroot(lambda t: thd(t) - mp.mpf(hi), mp.mpf(hi))
+        C = [mp.mpf(x) for x in rp[:17]]
+        S = [mp.mpf(x) for x in rp[17:34]]
+        worst = gworst = mp.mpf(0)
+        ts = [mp.mpf(0), th_max] + [th_max * mp.mpf(float(u)) for u in rng.uniform(0, 1, 1498)]
+        for t in ts:
+            ru = thd(t)
+            s = ru * ru
+            pc = mp.polyval(C[::-1], s)
+            ps = mp.polyval(S[::-1], s)
+            worst = max(worst, abs(pc - mp.cos(t)), abs(ru * ps - mp.sin(t)))
+            gworst = max(gworst, abs(ru * mp.polyval(G[::-1], s) - t))
+        assert worst <= bound, (p, float(worst), bound)
+        assert 0 < gworst <= gbound, (p, float(gworst), gbound)
+        checked += 1
+        if p is KB_SAMPLE:
+            assert mode == 3 and bound <= 1e-13 and float(worst) <= bound
+    assert checked >= 6

@@ -246,3 +246,73 @@ extern "C" int acm_probe_write_sample(int variant, void* uv, void* xyz, uint64_t
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// ---------------------------------------------------------------------------
+// acm_probe_reproj: the traffic of k_reproj_pass1 (compute_reprojection_error,
+// DESIGN.md 8) with no camera model -- AoS xyz (24 B) + a 16-B observation
+// read per point, software-pipelined in A static slots exactly like the real
+// kernel, and (STORE) one 8-B value written per point (NTS: non-temporal).
+// STORE = false is the normal-equations kernel's pure read stream in the
+// same loop shape.  Driven by tools/diag_reproj_ceiling.py.
+namespace {
+
+template <int A, bool STORE, bool NTS>
+__global__ __launch_bounds__(256) void k_reproj_mimic(size_t n, const double* __restrict__ xyz,
+                                                      const double* __restrict__ obs,
+                                                      double* __restrict__ err,
+                                                      double* __restrict__ out) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    double xs[A], ys[A], zs[A];
+    dbl2 os[A];
+    auto load_slot = [&](int q, size_t iq) {
+        const size_t ic = iq < n ? iq : n - 1;
+        xs[q] = __builtin_nontemporal_load(xyz + 3 * ic);
+        ys[q] = __builtin_nontemporal_load(xyz + 3 * ic + 1);
+        zs[q] = __builtin_nontemporal_load(xyz + 3 * ic + 2);
+        os[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(obs) + ic);
+    };
+    double s = 0.0;
+    if (n) {
+#pragma unroll
+        for (int q = 0; q < A; ++q) load_slot(q, i + (size_t)q * stride);
+    }
+    for (; i < n; i += (size_t)A * stride) {
+#pragma unroll
+        for (int q = 0; q < A; ++q) {
+            const size_t iq = i + (size_t)q * stride;
+            if (iq < n) {
+                const double e = xs[q] * zs[q] + ys[q] - os[q].x * os[q].y;
+                s += e;
+                if (STORE) {
+                    if (NTS) __builtin_nontemporal_store(e, err + iq);
+                    else err[iq] = e;
+                }
+            }
+            load_slot(q, iq + (size_t)A * stride);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) out[(size_t)blockIdx.x * 4 + (threadIdx.x >> 6)] = s;
+}
+
+}  // namespace
+
+// store: 0 = none, 1 = non-temporal 8-B stores, 2 = plain 8-B stores
+extern "C" int acm_probe_reproj(size_t n, const double* xyz, const double* obs, double* err,
+                                double* out, int grid, int slots, int store, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+#define RP(AA)                                                                               \
+    if (slots == AA) {                                                                       \
+        if (store == 0) hipLaunchKernelGGL((k_reproj_mimic<AA, false, false>), dim3(grid), dim3(256), \
+                                           0, s, n, xyz, obs, err, out);                     \
+        else if (store == 1) hipLaunchKernelGGL((k_reproj_mimic<AA, true, true>), dim3(grid),  \
+                                                dim3(256), 0, s, n, xyz, obs, err, out);     \
+        else hipLaunchKernelGGL((k_reproj_mimic<AA, true, false>), dim3(grid), dim3(256), 0, s, n, \
+                                xyz, obs, err, out);                                         \
+        return (int)hipGetLastError();                                                       \
+    }
+    RP(2) RP(4) RP(6)
+#undef RP
+    return -1;
+}
