@@ -2822,6 +2822,11 @@ struct LinRows<ACM_RADTAN> {  // rad_tan.rs:168-198, k = 3
 };
 
 constexpr int kTsqrMaxBlocks = 2048;
+// non-temporal loads of the read-once point / observation streams in k_tsqr
+#ifndef ACM_TSQR_NTL
+#define ACM_TSQR_NTL 1
+#endif
+constexpr bool kTsqrNtl = ACM_TSQR_NTL != 0;
 template <int M> constexpr int kTsqrB = M <= 3 ? 4 : 2;
 
 // TagR != void (acm_linear_estimation_with_error, r04): the same pass also
@@ -2830,7 +2835,7 @@ template <int M> constexpr int kTsqrB = M <= 3 ? 4 : 2;
 // correspondences (camera_converter.rs:371-375) -- so the 40 B per point are
 // read once for both: per-point errors (errs), k_reproj_pass1's statistics
 // partials (rparts) and the median's pass-0 histogram (hparts).
-template <int MODEL, int LAYOUT, class TagR = void, bool NTS = false>
+template <int MODEL, int LAYOUT, class TagR = void, bool NTS = false, bool NTL = false>
 __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
                                                  const double* __restrict__ pts,
                                                  const double* __restrict__ obs,
@@ -2855,47 +2860,54 @@ __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
     for (int q = 0; q < S; ++q) R[q] = 0.0;
     int err = 0;
     const size_t stride = (size_t)gridDim.x * kBlock;
-    // kTsqrB<M> points per lane step (their loads in flight together), their
-    // 2 kTsqrB rows folded in with one Householder reflection per column
+    // kTsqrB<M> points per lane step, their 2 kTsqrB rows folded in with one
+    // Householder reflection per column.  Software pipelined (r05) like
+    // k_normal_eq / k_reproj_pass1: B static slots, each slot's next point
+    // loaded as soon as the slot's current one is consumed, so the next
+    // step's B points are in flight while this step's Householder runs
+    // (branch-free loads; past the end: point n - 1 again, never used).
+    // The r04 form loaded B points, then computed, with no loads in flight
+    // across the step: 1.00 ms at 92.9M for the fused opening, whose
+    // traffic's ceiling is ~0.80 ms (profiles/r05m_reproj_ceiling.log).
     constexpr int B = kTsqrB<M>;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)B * stride) {
-        double x[B], y[B], z[B];
-        double2 o[B];
+    double xs[B], ys[B], zs[B];
+    double2 os[B];
+    auto load_slot = [&](int q, size_t iq) {
+        const size_t ic = iq < n ? iq : n - 1;
+        load_point<LAYOUT, NTL>(pts, n, ic, xs[q], ys[q], zs[q]);
+        os[q] = ld2<NTL>(obs + 2 * ic);
+    };
+    size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (n) {
+#pragma unroll
+        for (int q = 0; q < B; ++q) load_slot(q, i + (size_t)q * stride);
+    }
+    for (; i < n; i += (size_t)B * stride) {
+        double rows[2 * B][M];
 #pragma unroll
         for (int b = 0; b < B; ++b) {
             const size_t ib = i + (size_t)b * stride;
-            const size_t ic = ib < n ? ib : n - 1;
-            load_point<LAYOUT>(pts, n, ic, x[b], y[b], z[b]);
-            o[b] = *reinterpret_cast<const double2*>(obs + 2 * ic);
-        }
-        if constexpr (REPROJ) {
-            using MR = typename TagR::template type<double>;
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const size_t ib = i + (size_t)b * stride;
-                const bool in = ib < n;
+            const bool in = ib < n;
+            if constexpr (REPROJ) {
+                using MR = typename TagR::template type<double>;
                 double e = __builtin_nan("");
                 if (in) {
-                    e = reproj_error<MR>(c, x[b], y[b], z[b], o[b]);
+                    e = reproj_error<MR>(c, xs[b], ys[b], zs[b], os[b]);
                     acc.add(e);
                     if (NTS) __builtin_nontemporal_store(e, errs + ib);
                     else errs[ib] = e;
                 }
                 sel_count<true>(h, in, sel_digit0(e));
             }
-        }
-        double rows[2 * B][M];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const bool in = i + (size_t)b * stride < n;
             int e = 0;
-            const bool ok = in && RW::rows(c, x[b], y[b], z[b], o[b].x, o[b].y, rows[2 * b],
+            const bool ok = in && RW::rows(c, xs[b], ys[b], zs[b], os[b].x, os[b].y, rows[2 * b],
                                            rows[2 * b + 1], e);
             if (in) err |= e;
             if (!ok) {
 #pragma unroll
                 for (int q = 0; q < M; ++q) rows[2 * b][q] = rows[2 * b + 1][q] = 0.0;
             }
+            load_slot(b, ib + (size_t)B * stride);
         }
         tri_add_rows<M, 2 * B>(R, rows);
     }
@@ -4916,7 +4928,8 @@ ACM_API int acm_linear_system_qr(const acm_camera* cam, size_t n, const double* 
     auto go = [&](auto model_c) {
         constexpr int MOD = decltype(model_c)::value;
         constexpr int M = LinRows<MOD>::K + 1;
-        auto kern = layout == ACM_LAYOUT_AOS ? k_tsqr<MOD, ACM_LAYOUT_AOS> : k_tsqr<MOD, ACM_LAYOUT_SOA>;
+        auto kern = layout == ACM_LAYOUT_AOS ? k_tsqr<MOD, ACM_LAYOUT_AOS, void, false, kTsqrNtl>
+                                             : k_tsqr<MOD, ACM_LAYOUT_SOA, void, false, kTsqrNtl>;
         const int nb = std::min((int)tsqr_blocks(n),
                                 resident_blocks(reinterpret_cast<const void*>(kern)));
         hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
@@ -4968,8 +4981,8 @@ int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points
         constexpr int MOD = decltype(model_c)::value;
         using TagR = decltype(tag);
         constexpr int M = LinRows<MOD>::K + 1;
-        auto kern = layout == ACM_LAYOUT_AOS ? k_tsqr<MOD, ACM_LAYOUT_AOS, TagR, true>
-                                             : k_tsqr<MOD, ACM_LAYOUT_SOA, TagR, true>;
+        auto kern = layout == ACM_LAYOUT_AOS ? k_tsqr<MOD, ACM_LAYOUT_AOS, TagR, true, kTsqrNtl>
+                                             : k_tsqr<MOD, ACM_LAYOUT_SOA, TagR, true, kTsqrNtl>;
         nb = std::min((int)tsqr_blocks(n), resident_blocks(reinterpret_cast<const void*>(kern)));
         hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
                            points_2d, parts, error_flag, errs, p1, hparts);

@@ -89,7 +89,13 @@ def durations(kt_dir):
             (int(r["Dispatch_Id"]),
              (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
         res[(short(r["Kernel_Name"]), grid)] = {
-            "vgprs": int(r.get("VGPR_Count") or 0), "agprs": int(r.get("Accum_VGPR_Count") or 0),
+            # rocprofv3 (ROCm 7.2) reports gfx950 wave64 VGPR_Count as HALF the
+            # allocated registers: k_tsqr<DS, +error> 52 vs the compiler's 104
+            # (-Rpass-analysis=kernel-resource-usage, occupancy 4), KB normal
+            # equations 68 vs 134 (occupancy 3), k_fov_grid_pl 80 vs 153 -- so
+            # the allocation is taken as twice the trace's figure
+            "vgprs": 2 * int(r.get("VGPR_Count") or 0),
+            "agprs": 2 * int(r.get("Accum_VGPR_Count") or 0),
             "sgprs": int(r.get("SGPR_Count") or 0), "lds_bytes": int(r.get("LDS_Block_Size") or 0),
             "block": int(r.get("Workgroup_Size_X") or 0)}
     out, classes = {}, {}

@@ -8,6 +8,7 @@ zero-compute probes of their exact traffic:
   real  normal_eq       acm_normal_equations (40 B read per point)
   real  opening         acm_linear_estimation_with_error (initial error +
                         TSQR in one read, the median, the host solve)
+  real  tsqr            acm_linear_system_qr (TSQR of [A | b] alone, 40 B read)
   probe reproj_A{2,4,6}_{none,nt,plain}_g{grid}
                         tools/hbm_probe.hip acm_probe_reproj: the same loads in
                         the same static-slot pipeline, one 8-B store per point
@@ -85,6 +86,9 @@ def main():
             L.acm_reprojection_error.argtypes = [vp, sz, vp, ci, vp, vp, vp, vp, sz, vp]
             L.acm_normal_equations.argtypes = [vp, sz, vp, ci, vp, ci, vp, vp, sz, vp]
             L.acm_linear_estimation_with_error.argtypes = [vp, sz, vp, ci, vp, vp, vp, sz, vp]
+            L.acm_linear_system_qr_workspace_size.argtypes = [ci, sz]
+            L.acm_linear_system_qr_workspace_size.restype = sz
+            L.acm_linear_system_qr.argtypes = [vp, sz, vp, ci, vp, vp, vp, vp, sz, vp]
             libs.append((os.path.relpath(os.path.abspath(path), ROOT), L))
 
         def cam(L, params):
@@ -98,7 +102,9 @@ def main():
         res = torch.empty((80,), dtype=torch.float64, device="cuda")
         wsb = max(max(L.acm_reprojection_error_workspace_size(n),
                       L.acm_normal_equations_workspace_size(3, n),
-                      L.acm_linear_estimation_with_error_workspace_size(3, n)) for _, L in libs)
+                      L.acm_linear_estimation_with_error_workspace_size(3, n),
+                      L.acm_linear_system_qr_workspace_size(3, n)) for _, L in libs)
+        eflag = torch.zeros((4,), dtype=torch.int32, device="cuda")
         ws = torch.empty(((wsb + 7) // 8,), dtype=torch.float64, device="cuda")
         init = [240.0, 240.0, 256.0, 256.0, 0.5, 0.1]  # _init_target's DS start
 
@@ -123,9 +129,12 @@ def main():
                     ctypes.byref(c), n, xyz.data_ptr(), 0, uv.data_ptr(), 0, res.data_ptr(),
                     ws.data_ptr(), wsb, sh)),
                 "opening": (48, opening),
+                "tsqr": (40, lambda: L.acm_linear_system_qr(
+                    ctypes.byref(c0), n, xyz.data_ptr(), 0, uv.data_ptr(), res.data_ptr(),
+                    eflag.data_ptr(), ws.data_ptr(), wsb, sh)),
             }
         per_lib = [(tag, calls(L)) for tag, L in libs]
-        for name in ("reproj_stats", "reproj_error", "normal_eq", "opening"):
+        for name in ("reproj_stats", "reproj_error", "normal_eq", "opening", "tsqr"):
             best = {}
             for rnd in range(a.rounds):
                 for tag, cs in (per_lib if rnd % 2 == 0 else per_lib[::-1]):
