@@ -684,7 +684,12 @@ __global__ __launch_bounds__(kBlock) void k_round_trip(CamArg cam, size_t n,
 #ifndef ACM_AB_RT_NO_STATUS  // timing-only A/B build: the cost of the byte stores
             st1<NT>(pstatus + i, sp);
 #endif
-            st = M::unproject(c, u, v, X, Y, Z);
+            // RadTan: the pixel is one its own project() kept (same bounds
+            // test) or NaN, so the unprojection's bounds test is known false
+            if constexpr (std::is_same<M, RadTan<double>>::value)
+                st = M::template unproject<true>(c, u, v, X, Y, Z);
+            else
+                st = M::unproject(c, u, v, X, Y, Z);
             if (st != ST_OK) X = Y = Z = __builtin_nan("");
         }
         if (LAYOUT == ACM_LAYOUT_AOS) {
