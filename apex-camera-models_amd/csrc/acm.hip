@@ -1531,9 +1531,26 @@ __global__ __launch_bounds__(kBlock) void k_errstats_pass1(size_t n,
     reproj_block_store(s, ss, mn, mx, v, parts + (size_t)blockIdx.x * kReprojW);
 }
 
-// fixed-order finish: tot = [sum, sumsq, min, max, count, mean, M2]
-__global__ __launch_bounds__(kBlock) void k_reproj_finish1(const double* __restrict__ parts,
-                                                           int nb, double* __restrict__ tot) {
+// The median's selection state and workspace (acm_median_workspace_size):
+// [SelState x 2 | hist 2 x kSelBins f64 | candidate count u64 (+ 8 B) |
+// candidates].  Defined with the median below.
+struct SelState;
+struct SelWs {
+    SelState* st;
+    double* hist;
+    unsigned long long* count;
+    double* cbuf;
+};
+__device__ void sel_init_wg(const SelWs& w, unsigned long long m);
+
+// Fixed-order finish of the statistics partials, one workgroup:
+// tot = [sum, sumsq, min, max, count, mean, M2], then (r05: one launch
+// instead of two) result = [rmse, min, max, mean, stddev, n_valid, sum,
+// sumsq]; with sel.st != nullptr also the median's initial state for
+// n_valid = count (what k_sel_init would do after it, a third launch).
+__global__ __launch_bounds__(kBlock) void k_reproj_finish(const double* __restrict__ parts,
+                                                          int nb, double* __restrict__ tot,
+                                                          double* __restrict__ out, SelWs sel) {
     double s = 0, ss = 0, mn = INFINITY, mx = -INFINITY;
     Mv v{0.0, 0.0, 0.0};
     for (int b = threadIdx.x; b < nb; b += kBlock) {
@@ -1541,22 +1558,25 @@ __global__ __launch_bounds__(kBlock) void k_reproj_finish1(const double* __restr
         s += p[0]; ss += p[1]; mn = fmin(mn, p[2]); mx = fmax(mx, p[3]);
         v = mv_merge(v, Mv{p[4], p[5], p[6]});
     }
-    reproj_block_store(s, ss, mn, mx, v, tot);
-}
-
-// result = [rmse, min, max, mean, stddev, n_valid, sum, sumsq]
-__global__ void k_reproj_final(const double* __restrict__ tot, double* __restrict__ out) {
-    if (threadIdx.x != 0) return;
-    const double nn = tot[4];
-    const double mean = tot[0] / nn;  // error_metrics.rs:88-89: sum / n
-    out[0] = sqrt(tot[1] / nn);
-    out[1] = tot[2];
-    out[2] = tot[3];
-    out[3] = mean;
-    out[4] = sqrt(fmax(tot[6], 0.0) / nn);
-    out[5] = nn;
-    out[6] = tot[0];
-    out[7] = tot[1];
+    reproj_block_store(s, ss, mn, mx, v, tot);  // thread 0 writes tot
+    __shared__ double s_nn;
+    if (threadIdx.x == 0) {  // its own writes: no fence needed
+        const double nn = tot[4];
+        const double mean = tot[0] / nn;  // error_metrics.rs:88-89: sum / n
+        out[0] = sqrt(tot[1] / nn);
+        out[1] = tot[2];
+        out[2] = tot[3];
+        out[3] = mean;
+        out[4] = sqrt(fmax(tot[6], 0.0) / nn);
+        out[5] = nn;
+        out[6] = tot[0];
+        out[7] = tot[1];
+        s_nn = nn;
+    }
+    if (sel.st) {
+        __syncthreads();
+        sel_init_wg(sel, (unsigned long long)s_nn);
+    }
 }
 
 // ------------------------------------------------------------ sample_points
@@ -2607,13 +2627,13 @@ __global__ __launch_bounds__(kSelBlock) void k_sel_compact(size_t n, const doubl
 }
 
 // Picks this pass's digit for both states from the (all-reduced) histograms
-// and clears them for the next pass.  One workgroup: each lane owns 8
-// consecutive bins, a block-wide inclusive scan finds the bin where the
-// running count passes k.
-__global__ __launch_bounds__(kBlock) void k_sel_pick(SelState* __restrict__ st, int pass,
-                                                     double* __restrict__ hist) {
-    constexpr int PER = kSelBins / kBlock;
-    __shared__ unsigned long long scan[kBlock];
+// and clears them for the next pass.  One workgroup of NT lanes: each lane
+// owns kSelBins / NT consecutive bins, a block-wide inclusive scan finds the
+// bin where the running count passes k.
+template <int NT>
+__device__ __forceinline__ void sel_pick_wg(SelState* st, int pass, double* hist) {
+    constexpr int PER = kSelBins / NT;
+    __shared__ unsigned long long scan[NT];
     __shared__ int found;
     const int t = threadIdx.x;
     const int shift = sel_shift(pass);
@@ -2624,9 +2644,9 @@ __global__ __launch_bounds__(kBlock) void k_sel_pick(SelState* __restrict__ st, 
 #pragma unroll
         for (int j = 0; j < PER; ++j) mine += (unsigned long long)hw[t * PER + j];
         scan[t] = mine;
-        if (t == 0) found = kBlock - 1;
+        if (t == 0) found = NT - 1;
         __syncthreads();
-        for (int off = 1; off < kBlock; off <<= 1) {  // Hillis-Steele inclusive scan
+        for (int off = 1; off < NT; off <<= 1) {  // Hillis-Steele inclusive scan
             const unsigned long long v = t >= off ? scan[t - off] : 0;
             __syncthreads();
             scan[t] += v;
@@ -2650,35 +2670,45 @@ __global__ __launch_bounds__(kBlock) void k_sel_pick(SelState* __restrict__ st, 
         }
         __syncthreads();
     }
-    for (int j = t; j < 2 * kSelBins; j += kBlock) hist[j] = 0.0;
+    for (int j = t; j < 2 * kSelBins; j += NT) hist[j] = 0.0;
 }
 
-__global__ void k_sel_init(SelState* __restrict__ st, const double* __restrict__ nvalid_src,
-                           unsigned long long nvalid_fixed, double* __restrict__ hist,
-                           unsigned long long* __restrict__ count) {
-    const unsigned long long m =
-        nvalid_src ? (unsigned long long)nvalid_src[0] : nvalid_fixed;
+__global__ __launch_bounds__(kBlock) void k_sel_pick(SelState* __restrict__ st, int pass,
+                                                     double* __restrict__ hist) {
+    sel_pick_wg<kBlock>(st, pass, hist);
+}
+
+// state a: rank (m - 1) / 2, state b: rank m / 2 (equal for odd m); zero
+// histograms and candidate count.  Every lane of one workgroup.
+__device__ void sel_init_wg(const SelWs& w, unsigned long long m) {
     if (threadIdx.x == 0) {
-        *count = 0;
-        // state a: rank (m-1)/2 ; state b: rank m/2  (equal for odd m)
-        st[0].k = m ? (m - 1) / 2 : 0;
-        st[1].k = m / 2;
-        st[0].prefix = st[1].prefix = 0;
-        st[0].mask = st[1].mask = 0;
+        *w.count = 0;
+        w.st[0].k = m ? (m - 1) / 2 : 0;
+        w.st[1].k = m / 2;
+        w.st[0].prefix = w.st[1].prefix = 0;
+        w.st[0].mask = w.st[1].mask = 0;
     }
-    for (int j = threadIdx.x; j < 2 * kSelBins; j += blockDim.x) hist[j] = 0.0;
+    for (int j = threadIdx.x; j < 2 * kSelBins; j += blockDim.x) w.hist[j] = 0.0;
+}
+
+__global__ void k_sel_init(SelWs w, const double* __restrict__ nvalid_src,
+                           unsigned long long nvalid_fixed) {
+    sel_init_wg(w, nvalid_src ? (unsigned long long)nvalid_src[0] : nvalid_fixed);
+}
+
+__device__ void sel_finish_one(const SelState* a, const SelState* b, unsigned long long m,
+                               double* out) {
+    const double va = __longlong_as_double((long long)a->prefix);
+    const double vb = __longlong_as_double((long long)b->prefix);
+    if (m == 0) out[0] = __builtin_nan("");
+    else out[0] = (m % 2 == 0) ? (va + vb) / 2.0 : vb;
 }
 
 __global__ void k_sel_finish(const SelState* __restrict__ a, const SelState* __restrict__ b,
                              const double* __restrict__ nvalid_src,
                              unsigned long long nvalid_fixed, double* __restrict__ out) {
     if (threadIdx.x != 0) return;
-    const unsigned long long m =
-        nvalid_src ? (unsigned long long)nvalid_src[0] : nvalid_fixed;
-    const double va = __longlong_as_double((long long)a->prefix);
-    const double vb = __longlong_as_double((long long)b->prefix);
-    if (m == 0) out[0] = __builtin_nan("");
-    else out[0] = (m % 2 == 0) ? (va + vb) / 2.0 : vb;
+    sel_finish_one(a, b, nvalid_src ? (unsigned long long)nvalid_src[0] : nvalid_fixed, out);
 }
 
 // ------------------------------------------------------ linear estimation
@@ -2832,6 +2862,14 @@ constexpr int kTsqrMaxBlocks = 2048;
 #define ACM_TSQR_NTL 1
 #endif
 constexpr bool kTsqrNtl = ACM_TSQR_NTL != 0;
+// Householder batches per round of load slots (k_tsqr): the loads of this
+// many batches are in flight at once (2 vs 1 at 92.9M, same box: the fused
+// opening 1.157 -> 1.144 ms, TSQR alone 0.583 -> 0.580 ms,
+// profiles/r05p_tsqr_rounds_ab.log; bit-identical, the fold order is the same)
+#ifndef ACM_TSQR_ROUNDS
+#define ACM_TSQR_ROUNDS 2
+#endif
+constexpr int kTsqrRounds = ACM_TSQR_ROUNDS;
 template <int M> constexpr int kTsqrB = M <= 3 ? 4 : 2;
 
 // TagR != void (acm_linear_estimation_with_error, r04): the same pass also
@@ -2875,8 +2913,9 @@ __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
     // across the step: 1.00 ms at 92.9M for the fused opening, whose
     // traffic's ceiling is ~0.80 ms (profiles/r05m_reproj_ceiling.log).
     constexpr int B = kTsqrB<M>;
-    double xs[B], ys[B], zs[B];
-    double2 os[B];
+    constexpr int A = B * kTsqrRounds;  // load slots: kTsqrRounds batches in flight
+    double xs[A], ys[A], zs[A];
+    double2 os[A];
     auto load_slot = [&](int q, size_t iq) {
         const size_t ic = iq < n ? iq : n - 1;
         load_point<LAYOUT, NTL>(pts, n, ic, xs[q], ys[q], zs[q]);
@@ -2885,12 +2924,15 @@ __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
     size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
     if (n) {
 #pragma unroll
-        for (int q = 0; q < B; ++q) load_slot(q, i + (size_t)q * stride);
+        for (int q = 0; q < A; ++q) load_slot(q, i + (size_t)q * stride);
     }
-    for (; i < n; i += (size_t)B * stride) {
+    for (; i < n; i += (size_t)A * stride) {
+#pragma unroll
+      for (int g = 0; g < kTsqrRounds; ++g) {
         double rows[2 * B][M];
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
+        for (int bb = 0; bb < B; ++bb) {
+            const int b = g * B + bb;  // slot
             const size_t ib = i + (size_t)b * stride;
             const bool in = ib < n;
             if constexpr (REPROJ) {
@@ -2905,16 +2947,17 @@ __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
                 sel_count<true>(h, in, sel_digit0(e));
             }
             int e = 0;
-            const bool ok = in && RW::rows(c, xs[b], ys[b], zs[b], os[b].x, os[b].y, rows[2 * b],
-                                           rows[2 * b + 1], e);
+            const bool ok = in && RW::rows(c, xs[b], ys[b], zs[b], os[b].x, os[b].y, rows[2 * bb],
+                                           rows[2 * bb + 1], e);
             if (in) err |= e;
             if (!ok) {
 #pragma unroll
-                for (int q = 0; q < M; ++q) rows[2 * b][q] = rows[2 * b + 1][q] = 0.0;
+                for (int q = 0; q < M; ++q) rows[2 * bb][q] = rows[2 * bb + 1][q] = 0.0;
             }
-            load_slot(b, ib + (size_t)B * stride);
+            load_slot(b, ib + (size_t)A * stride);
         }
         tri_add_rows<M, 2 * B>(R, rows);
+      }
     }
     // wave merge (fixed butterfly order)
 #pragma unroll
@@ -4525,10 +4568,14 @@ ACM_API size_t acm_reprojection_stats_workspace_size(size_t n) {
 
 // hparts != nullptr: also the median's first histogram per workgroup
 // (k_reproj_pass1<HIST>); *nb_out = the workgroups launched
+static SelWs sel_ws(void* workspace);
+// median_ws != nullptr: the finish kernel also initialises that median
+// workspace for n_valid (acm_reprojection_error)
 static int reprojection_stats_impl(const acm_camera* cam, size_t n, const double* points_3d,
                                    int layout, const double* points_2d, double* result,
                                    double* errors, void* workspace, hipStream_t s,
-                                   unsigned int* hparts, int* nb_out) {
+                                   unsigned int* hparts, int* nb_out,
+                                   void* median_ws = nullptr) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -4560,8 +4607,8 @@ static int reprojection_stats_impl(const acm_camera* cam, size_t n, const double
         };
         if (layout == ACM_LAYOUT_AOS) go(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else go(std::integral_constant<int, ACM_LAYOUT_SOA>{});
-        hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb1, tot);
-        hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, result);
+        hipLaunchKernelGGL(k_reproj_finish, dim3(1), dim3(kBlock), 0, s, p1, nb1, tot, result,
+                           median_ws ? sel_ws(median_ws) : SelWs{});
         if (nb_out) *nb_out = nb1;
         return check_launch("acm_reprojection_stats");
     });
@@ -4594,8 +4641,7 @@ ACM_API int acm_error_stats(size_t n, const double* errors, double* result, void
     nb = std::max(1, std::min(nb, resident_blocks(reinterpret_cast<const void*>(k_errstats_pass1))));
     double* tot = p1 + (size_t)nb * kReprojW;
     hipLaunchKernelGGL(k_errstats_pass1, dim3(nb), dim3(kBlock), 0, s, n, errors, p1);
-    hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb, tot);
-    hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, result);
+    hipLaunchKernelGGL(k_reproj_finish, dim3(1), dim3(kBlock), 0, s, p1, nb, tot, result, SelWs{});
     return check_launch("acm_error_stats");
 }
 
@@ -4956,7 +5002,8 @@ static size_t reproj_error_median_offset(size_t n);
 static int median_impl(size_t n, const double* values, const double* n_valid_device,
                        uint64_t n_valid, double* out, void* workspace,
                        acm_allreduce_fn allreduce, void* allreduce_ctx, void* stream,
-                       const unsigned int* hparts, int hnb);
+                       const unsigned int* hparts, int hnb, bool inited);
+static SelWs sel_ws(void* workspace);
 
 extern "C++" {
 namespace acm {
@@ -5004,12 +5051,12 @@ int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points
     case ACM_UCM: go(std::integral_constant<int, ACM_UCM>{}, Tag<Ucm>{}); break;
     default: go(std::integral_constant<int, ACM_EUCM>{}, Tag<Eucm>{}); break;
     }
-    hipLaunchKernelGGL(k_reproj_finish1, dim3(1), dim3(kBlock), 0, s, p1, nb, tot);
-    hipLaunchKernelGGL(k_reproj_final, dim3(1), dim3(64), 0, s, tot, result);
+    void* mws = (char*)ws_err + reproj_error_median_offset(n);
+    hipLaunchKernelGGL(k_reproj_finish, dim3(1), dim3(kBlock), 0, s, p1, nb, tot, result,
+                       sel_ws(mws));
     if ((rc = check_launch("acm_linear_estimation_with_error"))) return rc;
-    return median_impl(n, errs, result + 5, 0, result + 8,
-                       (char*)ws_err + reproj_error_median_offset(n), nullptr, nullptr, stream,
-                       hparts, nb);
+    return median_impl(n, errs, result + 5, 0, result + 8, mws, nullptr, nullptr, stream, hparts,
+                       nb, true);
 }
 }  // namespace acm
 }
@@ -5124,29 +5171,43 @@ ACM_API size_t acm_median_workspace_size(size_t n) {
 
 // hparts / hnb: pass 0's histogram already counted per workgroup by
 // k_reproj_pass1<HIST> (acm_reprojection_error): merged instead of read.
+static SelWs sel_ws(void* workspace) {
+    SelWs w;
+    w.st = (SelState*)workspace;
+    w.hist = (double*)(w.st + 2);
+    w.count = (unsigned long long*)(w.hist + 2 * kSelBins);
+    w.cbuf = (double*)(w.count + 2);
+    return w;
+}
+
+// inited: the caller's k_reproj_finish already ran sel_init_wg on this
+// workspace (acm_reprojection_error, acm_linear_estimation_with_error)
 static int median_impl(size_t n, const double* values, const double* n_valid_device,
                        uint64_t n_valid, double* out, void* workspace,
                        acm_allreduce_fn allreduce, void* allreduce_ctx, void* stream,
-                       const unsigned int* hparts, int hnb) {
+                       const unsigned int* hparts, int hnb, bool inited) {
     hipStream_t s = (hipStream_t)stream;
-    SelState* st = (SelState*)workspace;
-    double* hist = (double*)(st + 2);
-    unsigned long long* count = (unsigned long long*)(hist + 2 * kSelBins);
-    double* cbuf = (double*)(count + 2);
+    const SelWs w = sel_ws(workspace);
+    SelState* st = w.st;
+    double* hist = w.hist;
     // one 1024-lane workgroup per CU (fewer for small n)
     const unsigned nb = (unsigned)std::max<size_t>(
         1, std::min<size_t>((size_t)cu_count(), (n + kSelBlock * kSelU - 1) / (kSelBlock * kSelU)));
     const bool ntl = g_nt_loads != 0;
     // passes 0-1 read every value (pass 0 aggregates its exponent digits per
     // wave); then the candidates sharing either state's 22-bit prefix are
-    // compacted and passes 2-5 read only them.
+    // compacted and passes 2-5 read only them.  (Picking in the histogram
+    // kernels' last workgroup instead of a k_sel_pick launch was measured in
+    // r05: the ticket's fan-in and the fences cost more than the launches,
+    // reproj_error 1.10 -> 1.46 ms at 92.9M, profiles/r05q_median_ab.log.)
     constexpr int kFullPasses = 2;
-    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(kBlock), 0, s, st, n_valid_device,
-                       (unsigned long long)n_valid, hist, count);
+    if (!inited)
+        hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(kBlock), 0, s, w, n_valid_device,
+                           (unsigned long long)n_valid);
     for (int pass = 0; pass < kSelPasses; ++pass) {
         if (pass == kFullPasses)
             hipLaunchKernelGGL((ntl ? k_sel_compact<true> : k_sel_compact<false>), dim3(nb),
-                               dim3(kSelBlock), 0, s, n, values, st, cbuf, count);
+                               dim3(kSelBlock), 0, s, n, values, st, w.cbuf, w.count);
         if (pass == 0 && hparts)
             hipLaunchKernelGGL(k_sel_hist_merge, dim3(kSelBins / kBlock, kSelMergeG), dim3(kBlock),
                                0, s, hparts, hnb, hist);
@@ -5159,7 +5220,7 @@ static int median_impl(size_t n, const double* values, const double* n_valid_dev
                                hist);
         else
             hipLaunchKernelGGL((k_sel_hist<false, false>), dim3(nb), dim3(kSelBlock),
-                               0, s, (size_t)0, count, cbuf, st, pass, hist);
+                               0, s, (size_t)0, w.count, w.cbuf, st, pass, hist);
         if (allreduce) {  // every rank then picks the same digits
             int rc = check_launch("acm_median_valid (histogram)");
             if (rc) return rc;
@@ -5182,7 +5243,7 @@ ACM_API int acm_median_valid_allreduce(size_t n, const double* values,
     if (workspace_bytes < acm_median_workspace_size(n))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "median workspace too small");
     return median_impl(n, values, n_valid_device, n_valid, out, workspace, allreduce,
-                       allreduce_ctx, stream, nullptr, 0);
+                       allreduce_ctx, stream, nullptr, 0, false);
 }
 
 // compute_reprojection_error in one call: [errors n f64 (when the caller
@@ -5210,13 +5271,14 @@ ACM_API int acm_reprojection_error(const acm_camera* cam, size_t n, const double
     char* ws = (char*)workspace;
     unsigned int* hparts = (unsigned int*)(ws + reproj_error_hist_offset(n));
     int nb = 0;
+    void* mws = ws + reproj_error_median_offset(n);
     int rc = reprojection_stats_impl(cam, n, points_3d, layout, points_2d, result, errors,
-                                     workspace, (hipStream_t)stream, hparts, &nb);
+                                     workspace, (hipStream_t)stream, hparts, &nb, mws);
     if (rc) return rc;
     const double* errs = errors ? errors : (const double*)workspace;
     // n_valid from result[5] on the device: no host round trip in between
-    return median_impl(n, errs, result + 5, 0, result + 8, ws + reproj_error_median_offset(n),
-                       nullptr, nullptr, stream, hparts, nb);
+    return median_impl(n, errs, result + 5, 0, result + 8, mws, nullptr, nullptr, stream, hparts,
+                       nb, true);
 }
 
 ACM_API int acm_median_valid(size_t n, const double* values, const double* n_valid_device,
