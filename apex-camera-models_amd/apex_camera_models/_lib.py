@@ -111,6 +111,7 @@ EXPORTED_SYMBOLS = (
     "acm_reprojection_error",
     "acm_linear_estimation_with_error_workspace_size",
     "acm_linear_estimation_with_error",
+    "acm_linear_estimation_with_error_async",
     "acm_error_stats_workspace_size",
     "acm_error_stats",
     "acm_linear_system_columns",
@@ -217,6 +218,8 @@ def load():
     L.acm_linear_estimation_with_error_workspace_size.restype = sz
     L.acm_linear_estimation_with_error.argtypes = [cam_p, sz, vp, i, vp, vp, vp, sz, vp]
     L.acm_linear_estimation_with_error.restype = i
+    L.acm_linear_estimation_with_error_async.argtypes = [cam_p, sz, vp, i, vp, vp, vp, vp, sz, vp]
+    L.acm_linear_estimation_with_error_async.restype = i
     L.acm_sample_points_grid.argtypes = [ctypes.c_uint32, ctypes.c_uint32, sz,
                                          ctypes.POINTER(ctypes.c_uint32),
                                          ctypes.POINTER(ctypes.c_uint32)]

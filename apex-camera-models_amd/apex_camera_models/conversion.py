@@ -72,9 +72,12 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
         estimate = lambda m: D.distributed_linear_estimation(m, points_3d, points_2d, group)  # noqa: E731
     else:
         reproj = lambda m: util.compute_reprojection_error(m, points_3d, points_2d)  # noqa: E731
+    finish_initial = None
     if allreduce is None:
-        # the initial error and the linear estimation in one pass (r04)
-        initial = util.initial_error_and_linear_estimation(model, points_3d, points_2d)
+        # the initial error and the linear estimation in one pass (r04); its
+        # median completes on the stream while the LM starts (r05)
+        initial, finish_initial = util.initial_error_and_linear_estimation(
+            model, points_3d, points_2d, defer_median=True)
     else:
         initial = reproj(model)
         estimate(model)
@@ -97,6 +100,8 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
         status = "Linear Only"
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
+    if finish_initial is not None:
+        initial = finish_initial()
     final = reproj(model)
     # camera_converter.rs:425-438; failed regions come back as NaN (no raise)
     validation = util.validate_conversion_accuracy(model, input_model)

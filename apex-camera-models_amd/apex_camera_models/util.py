@@ -7,6 +7,7 @@ tensors.
 from __future__ import annotations
 
 import ctypes
+import dataclasses
 from dataclasses import dataclass
 
 import torch
@@ -105,12 +106,19 @@ def compute_reprojection_error(camera_model: CameraModel, points3d, points2d) ->
                            median=out[8], n_valid=n_valid)
 
 
-def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d) -> ProjectionError:
+def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d,
+                                        defer_median: bool = False):
     """convert_to_*'s opening (camera_converter.rs:371-375): the reprojection
     error of `model` as given, then `model.linear_estimation` -- for the TSQR
-    models one pass over the correspondences (acm_linear_estimation_with_error).
+    models one pass over the correspondences (acm_linear_estimation_with_error_async).
     Raises like the two calls in that order: ZeroProjectionPoints first, then
-    the estimation's InvalidParams / NumericalError."""
+    the estimation's InvalidParams / NumericalError.
+
+    defer_median=True (conversion.convert, r05): returns (error, finish) at
+    once, `error.median` NaN; the median is still running on the stream and
+    finish() returns the completed ProjectionError -- call it after the next
+    synchronising step (the LM), so no host round trip separates the opening
+    from the LM's first evaluation."""
     L = _lib.load()
     p3 = _as_device_f64(points3d, 3)
     p2 = _as_device_f64(points2d, 2)
@@ -123,13 +131,14 @@ def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d) 
     ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=p3.device)
     # NaN until written: an early error return of the C call leaves it so
     res = torch.full((9,), float("nan"), dtype=torch.float64, device=p3.device)
+    host = (ctypes.c_double * 8)(*([float("nan")] * 8))
     cam = model.acm_camera()
-    rc = L.acm_linear_estimation_with_error(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
-                                            p2.data_ptr(), res.data_ptr(), ws.data_ptr(),
-                                            ws_bytes, _stream_handle())
+    rc = L.acm_linear_estimation_with_error_async(ctypes.byref(cam), n, p3.data_ptr(),
+                                                  _lib.LAYOUT_AOS, p2.data_ptr(), res.data_ptr(),
+                                                  host, ws.data_ptr(), ws_bytes, _stream_handle())
     if rc not in (_lib.ACM_SUCCESS, _lib.ERR_INVALID_PARAMS, _lib.ERR_NUMERICAL):
         _lib.check(rc)
-    out = res.cpu().tolist()
+    out = list(host)
     if out[5] != out[5]:  # the initial error was never computed: the call's own error
         if rc == _lib.ERR_NUMERICAL:
             raise NumericalError(_lib.last_error())
@@ -142,8 +151,14 @@ def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d) 
     if rc == _lib.ERR_NUMERICAL:
         raise NumericalError(_lib.last_error())
     model._set_params(list(cam.params)[: model.NUM_PARAMS])
-    return ProjectionError(rmse=out[0], min=out[1], max=out[2], mean=out[3], stddev=out[4],
-                           median=out[8], n_valid=n_valid)
+    err = ProjectionError(rmse=out[0], min=out[1], max=out[2], mean=out[3], stddev=out[4],
+                          median=float("nan"), n_valid=n_valid)
+
+    def finish(err=err, res=res, ws=ws):  # ws: the median reads it until the stream passes
+        return dataclasses.replace(err, median=float(res[8].item()))
+    if defer_median:
+        return err, finish
+    return finish()
 
 
 def reprojection_median(errors: torch.Tensor, n_valid: int) -> float:

@@ -5012,9 +5012,14 @@ namespace acm {
 // reprojection error of *cam as given, then the factor merge, the error
 // statistics and the median follow on the stream.  ws_err is laid out as
 // acm_reprojection_error's workspace (errors first); result: its 9 f64.
+// host_out != nullptr (pinned, 25 f64; acm_linear_estimation_with_error_async):
+// right after the statistics -- before the median -- R and the flag (17 f64
+// from r_factor, the flag in r_factor[16]) and result[0..7] are copied there
+// and `ready` is recorded, so the host can solve while the median runs.
 int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                            const double* points_2d, double* r_factor, int* error_flag,
-                           double* result, void* ws_qr, void* ws_err, void* stream) {
+                           double* result, void* ws_qr, void* ws_err, void* stream,
+                           double* host_out, hipEvent_t ready) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -5055,6 +5060,14 @@ int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points
     hipLaunchKernelGGL(k_reproj_finish, dim3(1), dim3(kBlock), 0, s, p1, nb, tot, result,
                        sel_ws(mws));
     if ((rc = check_launch("acm_linear_estimation_with_error"))) return rc;
+    if (host_out) {
+        if (hipMemcpyAsync(host_out, r_factor, 17 * sizeof(double), hipMemcpyDeviceToHost, s) !=
+                hipSuccess ||
+            hipMemcpyAsync(host_out + 17, result, 8 * sizeof(double), hipMemcpyDeviceToHost, s) !=
+                hipSuccess ||
+            hipEventRecord(ready, s) != hipSuccess)
+            return check_launch("acm_linear_estimation_with_error (copy)");
+    }
     return median_impl(n, errs, result + 5, 0, result + 8, mws, nullptr, nullptr, stream, hparts,
                        nb, true);
 }

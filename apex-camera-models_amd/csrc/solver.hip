@@ -32,7 +32,8 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
                           unsigned int* ticket);
 int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                            const double* points_2d, double* r_factor, int* error_flag,
-                           double* result, void* ws_qr, void* ws_err, void* stream);
+                           double* result, void* ws_qr, void* ws_err, void* stream,
+                           double* host_out, hipEvent_t ready);
 }
 
 namespace {
@@ -291,16 +292,47 @@ ACM_API size_t acm_linear_estimation_with_error_workspace_size(int model, size_t
     return lin_err_qr_bytes(model, n) + 32 * sizeof(double) + err;
 }
 
-ACM_API int acm_linear_estimation_with_error(acm_camera* cam, size_t n, const double* points_3d,
-                                             int layout, const double* points_2d,
-                                             double* initial_error, void* workspace,
-                                             size_t workspace_bytes, void* stream) {
+// One pinned host buffer (R + flag + the 8 statistics) and one event per host
+// thread for the opening's early hand-off, freed when the thread exits.
+namespace {
+struct OpeningHost {
+    double* p = nullptr;
+    hipEvent_t ev = nullptr;
+    bool ok() {
+        if (!p) {
+            void* q = nullptr;
+            if (hipHostMalloc(&q, 32 * sizeof(double), hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                return false;
+            }
+            p = (double*)q;
+        }
+        if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            ev = nullptr;
+            return false;
+        }
+        return true;
+    }
+    ~OpeningHost() {
+        if (ev && hipEventDestroy(ev) != hipSuccess) (void)hipGetLastError();
+        if (p && hipHostFree(p) != hipSuccess) (void)hipGetLastError();
+    }
+};
+}  // namespace
+
+ACM_API int acm_linear_estimation_with_error_async(acm_camera* cam, size_t n,
+                                                   const double* points_3d, int layout,
+                                                   const double* points_2d, double* initial_error,
+                                                   double* initial_error_host, void* workspace,
+                                                   size_t workspace_bytes, void* stream) {
     if (!cam) return sfail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
     if (!initial_error) return sfail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
     const size_t need = acm_linear_estimation_with_error_workspace_size(cam->model, n);
     if (!need) return sfail(ACM_ERR_NOT_SUPPORTED, "model has no linear_estimation");
     if (!workspace || workspace_bytes < need)
         return sfail(ACM_ERR_WORKSPACE_TOO_SMALL, "linear-estimation workspace too small");
+    hipStream_t s = (hipStream_t)stream;
     const int k = acm_linear_system_columns(cam->model);
     // the reference computes initial_error first: it is written whatever the
     // estimation then does (FOV, or too few points: the two calls in order)
@@ -309,27 +341,48 @@ ACM_API int acm_linear_estimation_with_error(acm_camera* cam, size_t n, const do
                                         nullptr, workspace,
                                         acm_reprojection_error_workspace_size(n), stream);
         if (rc) return rc;
+        if (initial_error_host &&
+            (hip_ok(hipMemcpyAsync(initial_error_host, initial_error, 8 * sizeof(double),
+                                   hipMemcpyDeviceToHost, s)) ||
+             hip_ok(hipStreamSynchronize(s))))
+            return sfail(ACM_ERR_HIP, "linear estimation: device copy failed");
         return acm_linear_estimation(cam, n, points_3d, layout, points_2d, workspace,
                                      workspace_bytes, stream);
     }
-    const int M = k + 1, S = M * (M + 1) / 2;
+    static thread_local OpeningHost host;
+    if (!host.ok()) return sfail(ACM_ERR_HIP, "linear estimation: pinned buffer or event");
     const size_t qr = lin_err_qr_bytes(cam->model, n);
     double* d_r = (double*)((char*)workspace + qr);
     int* d_err = (int*)(d_r + 16);
     void* ws_err = (char*)workspace + qr + 32 * sizeof(double);
+    // R (<= 15 doubles), the flag (at double 16) and the statistics reach the
+    // host before the median runs (r05): the solve below overlaps it, and the
+    // median's result lands in initial_error[8] in stream order
     int rc = acm::linear_system_qr_error(cam, n, points_3d, layout, points_2d, d_r, d_err,
-                                         initial_error, workspace, ws_err, stream);
+                                         initial_error, workspace, ws_err, stream, host.p,
+                                         host.ev);
     if (rc) return rc;
-    // R (S <= 15 doubles) and the flag (at double 16) in one copy
-    double R[17];
-    hipStream_t s = (hipStream_t)stream;
-    (void)S;
-    if (hip_ok(hipMemcpyAsync(R, d_r, 17 * sizeof(double), hipMemcpyDeviceToHost, s)) ||
-        hip_ok(hipStreamSynchronize(s)))
+    if (hip_ok(hipEventSynchronize(host.ev)))
         return sfail(ACM_ERR_HIP, "linear estimation: device copy failed");
+    double R[17];
+    std::memcpy(R, host.p, sizeof(R));
+    if (initial_error_host) std::memcpy(initial_error_host, host.p + 17, 8 * sizeof(double));
     int err = 0;
     std::memcpy(&err, &R[16], sizeof(int));
     return acm_linear_estimation_solve(cam, n, R, err);
+}
+
+ACM_API int acm_linear_estimation_with_error(acm_camera* cam, size_t n, const double* points_3d,
+                                             int layout, const double* points_2d,
+                                             double* initial_error, void* workspace,
+                                             size_t workspace_bytes, void* stream) {
+    const int rc = acm_linear_estimation_with_error_async(cam, n, points_3d, layout, points_2d,
+                                                          initial_error, nullptr, workspace,
+                                                          workspace_bytes, stream);
+    // as before r05: everything, the median included, is done on return
+    if (hip_ok(hipStreamSynchronize((hipStream_t)stream)))
+        return sfail(ACM_ERR_HIP, "linear estimation: stream synchronize failed");
+    return rc;
 }
 
 ACM_API void acm_lm_default_config(acm_lm_config* cfg) {

@@ -285,6 +285,21 @@ ACM_API int acm_linear_estimation_with_error(acm_camera *cam, size_t n,
                                              const double *points_2d,
                                              double *initial_error, void *workspace,
                                              size_t workspace_bytes, void *stream);
+/* (r05) The same, returning as soon as *cam is estimated: the initial
+ * error's 8 statistics (acm_reprojection_stats' layout, n_valid at [5]) are
+ * copied to initial_error_host (nullable, host, 8 f64) before the median
+ * runs, the host solve overlaps the median, and the median itself lands in
+ * initial_error[8] in stream order (read it after a later synchronisation of
+ * `stream`; the workspace must stay allocated until then).  What
+ * conversion.convert uses, so the LM's first evaluation queues behind the
+ * median without a host round trip in between.  acm_linear_estimation_with_error
+ * is this call followed by a synchronisation of `stream`. */
+ACM_API int acm_linear_estimation_with_error_async(acm_camera *cam, size_t n,
+                                                   const double *points_3d, int layout,
+                                                   const double *points_2d,
+                                                   double *initial_error,
+                                                   double *initial_error_host, void *workspace,
+                                                   size_t workspace_bytes, void *stream);
 /* Multi-GPU linear_estimation: each rank runs acm_linear_system_qr on its
  * shard, the packed factors (host copies) are folded in rank order with
  * acm_linear_system_r_merge (Givens; R of the stacked rows), error flags

@@ -583,3 +583,52 @@ def test_linear_estimation_with_error_soa_layout(target):
         out.append((res.cpu().numpy(), list(cam.params)))
     assert np.array_equal(out[0][0], out[1][0])
     assert out[0][1] == out[1][1]
+
+
+@pytest.mark.parametrize("target", [DS, KB, FOV])
+def test_linear_estimation_with_error_async_matches_sync(target):
+    """acm_linear_estimation_with_error_async (r05): returns once the estimate
+    is solved, with the 8 initial-error statistics on the host and the median
+    completing in stream order -- the same statistics, median and estimate
+    bit for bit as the synchronous call (for FOV the two-call fallback), and
+    util's deferred form (conversion.convert) equal to its immediate one."""
+    import ctypes
+    import torch
+    from apex_camera_models import _lib, util
+    L = _lib.load()
+    uv, xyz, w, h = _sampled(KB, 300_000)
+    sp, _ = SAMPLES[KB]
+    init = {KB: sp[:4] + [0.0] * 4, DS: sp[:4] + [0.5, 0.1], FOV: sp[:4] + [1.0]}[target]
+    n = xyz.shape[0]
+    p3 = torch.as_tensor(xyz, device="cuda").contiguous()
+    p2 = torch.as_tensor(uv, device="cuda").contiguous()
+    sh = torch.cuda.current_stream().cuda_stream
+    wsb = L.acm_linear_estimation_with_error_workspace_size(target, n)
+    out = []
+    for asyn in (False, True):
+        cam = _model(target, init, w, h).acm_camera()
+        ws = torch.empty(((wsb + 7) // 8,), dtype=torch.float64, device="cuda")
+        res = torch.full((9,), float("nan"), dtype=torch.float64, device="cuda")
+        host = (ctypes.c_double * 8)(*([float("nan")] * 8))
+        if asyn:
+            _lib.check(L.acm_linear_estimation_with_error_async(
+                ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS, p2.data_ptr(),
+                res.data_ptr(), host, ws.data_ptr(), wsb, sh))
+            params = list(cam.params)  # final on return
+            stats = list(host)         # final on return
+        else:
+            _lib.check(L.acm_linear_estimation_with_error(
+                ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS, p2.data_ptr(),
+                res.data_ptr(), ws.data_ptr(), wsb, sh))
+            params, stats = list(cam.params), None
+        r = res.cpu().numpy()  # the stream has passed the median
+        if stats is not None:
+            assert np.array_equal(np.array(stats), r[:8]), (stats, r)
+        out.append((r, params))
+    assert np.array_equal(out[0][0], out[1][0]) and not np.isnan(out[1][0][8])
+    assert out[0][1] == out[1][1]
+    a, b = _model(target, init, w, h), _model(target, init, w, h)
+    e0 = util.initial_error_and_linear_estimation(a, p3, p2)
+    e1, finish = util.initial_error_and_linear_estimation(b, p3, p2, defer_median=True)
+    assert np.isnan(e1.median) and e1.n_valid == e0.n_valid
+    assert finish() == e0 and b.params() == a.params()
