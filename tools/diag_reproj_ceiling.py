@@ -9,6 +9,9 @@ zero-compute probes of their exact traffic:
   real  opening         acm_linear_estimation_with_error (initial error +
                         TSQR in one read, the median, the host solve)
   real  tsqr            acm_linear_system_qr (TSQR of [A | b] alone, 40 B read)
+  probe round_trip      acm_probe_round_trip: config 4's round-trip traffic (66 B per
+                        point at --rt-points, one point per lane) with no model,
+                        beside acm_project_unproject for Pinhole on the same points
   probe reproj_A{2,4,6}_{none,nt,plain}_g{grid}
                         tools/hbm_probe.hip acm_probe_reproj: the same loads in
                         the same static-slot pipeline, one 8-B store per point
@@ -38,6 +41,7 @@ def main():
     ap.add_argument("--libs", default="apex-camera-models_amd/lib/libacm.so")
     ap.add_argument("--only", default="real,probe")
     ap.add_argument("--grids", default="1024,2048")
+    ap.add_argument("--rt-points", type=int, default=50_000_000)
     a = ap.parse_args()
     only = set(a.only.split(","))
     import torch
@@ -141,6 +145,36 @@ def main():
                     best[tag] = min(best.get(tag, 1e9), timed(cs[name][1]))
             emit(name, best, per_lib[0][1][name][0])
         del errs, ws
+    if "rt" in only:
+        del uv, xyz
+        P = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libhbmprobe.so"))
+        P.acm_probe_round_trip.argtypes = [sz, vp, vp, vp, vp, vp, vp]
+        L = _lib.load()
+        m = a.rt_points
+        pts = samples.synthetic_points_device(m)
+        uv2 = torch.empty((m, 2), dtype=torch.float64, device="cuda")
+        st = torch.empty((m,), dtype=torch.uint8, device="cuda")
+        rays = torch.empty((m, 3), dtype=torch.float64, device="cuda")
+        st2 = torch.empty((m,), dtype=torch.uint8, device="cuda")
+        params, (pw, ph) = samples.SAMPLES[0]
+        cam = _lib.AcmCamera()
+        _lib.check(L.acm_camera_init(ctypes.byref(cam), 0, (ctypes.c_double * len(params))(
+            *params), len(params), pw, ph))
+        calls = {"probe": lambda: P.acm_probe_round_trip(m, pts.data_ptr(), uv2.data_ptr(),
+                                                         st.data_ptr(), rays.data_ptr(),
+                                                         st2.data_ptr(), sh),
+                 "pinhole": lambda: L.acm_project_unproject(ctypes.byref(cam), m, pts.data_ptr(), 0,
+                                                            uv2.data_ptr(), st.data_ptr(),
+                                                            rays.data_ptr(), st2.data_ptr(), sh)}
+        best = {}
+        for rnd in range(a.rounds):
+            for k, fn in (list(calls.items()) if rnd % 2 == 0 else list(calls.items())[::-1]):
+                best[k] = min(best.get(k, 1e9), timed(fn))
+        print(json.dumps({"call": "round_trip_traffic", "points": m,
+                          "ms": {k: round(v, 4) for k, v in best.items()},
+                          "TBps": {k: round(66 * m / v / 1e9, 2) for k, v in best.items()}}),
+              flush=True)
+        return
     if "probe" in only:
         P = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libhbmprobe.so"))
         P.acm_probe_reproj.argtypes = [sz, vp, vp, vp, vp, ci, ci, ci, vp]

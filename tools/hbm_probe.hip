@@ -316,3 +316,55 @@ extern "C" int acm_probe_reproj(size_t n, const double* xyz, const double* obs, 
 #undef RP
     return -1;
 }
+
+// ---------------------------------------------------------------------------
+// acm_probe_round_trip: the traffic of k_round_trip (config 4, one point per
+// lane) with no camera model: AoS xyz read (24 B), pixel pair (16 B) and
+// status byte written, then the AoS ray (24 B, LDS-staged into 16-B stores
+// per wave like the real kernel) and a second status byte.  66 B per point.
+namespace {
+
+__global__ __launch_bounds__(256) void k_rt_mimic(size_t n, const double* __restrict__ xyz,
+                                                  double* __restrict__ uv, uint8_t* __restrict__ st,
+                                                  double* __restrict__ rays,
+                                                  uint8_t* __restrict__ st2) {
+    __shared__ double s_ray[4][192];
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const size_t wfirst = i - lane;
+    if (wfirst >= n) return;
+    double x = 0.0, y = 0.0, z = 1.0;
+    if (i < n) {
+        x = xyz[3 * i];
+        y = xyz[3 * i + 1];
+        z = xyz[3 * i + 2];
+        put2<true>(uv + 2 * i, x + z, y + z);
+        __builtin_nontemporal_store((uint8_t)(z < 0.0), st + i);
+    }
+    if (wfirst + 64 <= n) {
+        double* sr = s_ray[wid];
+        sr[3 * lane] = x * 0.5;
+        sr[3 * lane + 1] = y * 0.5;
+        sr[3 * lane + 2] = z * 0.5;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double* dst = rays + 3 * wfirst;
+        put2<true>(dst + 2 * lane, sr[2 * lane], sr[2 * lane + 1]);
+        if (lane < 32) put2<true>(dst + 128 + 2 * lane, sr[128 + 2 * lane], sr[129 + 2 * lane]);
+    } else if (i < n) {
+        rays[3 * i] = x * 0.5;
+        rays[3 * i + 1] = y * 0.5;
+        rays[3 * i + 2] = z * 0.5;
+    }
+    if (i < n) __builtin_nontemporal_store((uint8_t)(z > 8.0), st2 + i);
+}
+
+}  // namespace
+
+extern "C" int acm_probe_round_trip(size_t n, const double* xyz, double* uv, uint8_t* st,
+                                    double* rays, uint8_t* st2, void* stream) {
+    hipLaunchKernelGGL(k_rt_mimic, dim3(blocks(n)), dim3(256), 0, (hipStream_t)stream, n, xyz, uv,
+                       st, rays, st2);
+    return (int)hipGetLastError();
+}
