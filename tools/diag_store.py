@@ -1,4 +1,4 @@
-"""Store ceiling of the sample_points write pass (DESIGN.md 5.4): write-only
+"""Store ceiling of the sample_points write pass (DESIGN.md 5.7): write-only
 kernels over the config-5 output shape, 92,935,075
 kept points x (16-B pixel + 24-B ray) = 3.72 GB (acm_probe_write_sample in
 tools/hbm_probe.hip, built by `make -C tools`), timed with HIP events on the

@@ -179,7 +179,7 @@ int acm_probe_mimic(size_t n, const double* xyz, double* uv, uint8_t* st, double
 
 // ---------------------------------------------------------------------------
 // acm_probe_write_sample: the store ceiling of the sample_points write pass
-// (DESIGN.md 5.4) -- write-only kernels in its output shape (a 16-B pixel
+// (DESIGN.md 5.7) -- write-only kernels in its output shape (a 16-B pixel
 // stream and a 24-B ray stream per kept point, 3.72 GB at config 5), no loads
 // and no arithmetic; driven by tools/diag_store.py.
 namespace {
