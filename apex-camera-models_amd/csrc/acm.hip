@@ -138,12 +138,23 @@ __host__ __device__ inline void unproject_consts(int model, const T* p, T* uk) {
         uk[1] = T(1) / (T(2) * p[8]);
     } else if (model == ACM_DOUBLE_SPHERE) {
         uk[0] = T(1) / (T(2) * p[4] - T(1));  // double_sphere.rs:205
+        // (r05) the projection condition's w2 (double_sphere.rs:177-184), a
+        // camera constant the reference evaluates per point: the same IEEE
+        // operations, so the same bits, once per camera
+        const T alpha = p[4], xi = p[5];
+        const T w1 = alpha <= T(0.5) ? alpha / (T(1) - alpha) : (T(1) - alpha) / alpha;
+        uk[1] = (w1 + xi) / sqrt(T(2) * w1 * xi + xi * xi + T(1));
     } else if (model == ACM_UCM) {
         const T gamma = T(1) - p[4];
         uk[0] = p[4] / gamma;                          // xi, ucm.rs:343
         uk[1] = gamma * gamma / (T(2) * p[4] - T(1));  // ucm.rs:180
+        // (r05) the projection condition's w (ucm.rs:154-161), per camera
+        uk[2] = p[4] <= T(0.5) ? p[4] / (T(1) - p[4]) : (T(1) - p[4]) / p[4];
     } else if (model == ACM_EUCM) {
         uk[0] = T(1) / p[5] * (T(2) * p[4] - T(1));  // eucm.rs:196 (precedence quirk)
+        // (r05) the projection condition's (alpha - 1) / (2 alpha - 1)
+        // (eucm.rs:167-177, used when alpha > 0.5), per camera
+        uk[1] = (p[4] - T(1)) / (T(2) * p[4] - T(1));
     }
 }
 
@@ -735,14 +746,16 @@ template <> struct UnprojectStaged<Tag<RadTan>> { static constexpr bool on = fal
 // profiles/r05d_round_trip_ab.log, best of 3 interleaved blocks): one point
 // per lane for Pinhole / UCM / EUCM (0.565 -> 0.553 ms) and for KB, whose
 // rays are now staged too (its VALU work fell with the SGPR-spill fix:
-// 0.608 -> 0.587); four per lane for DS (0.641 -> 0.626); RadTan keeps two,
-// direct stores (every setting within 1.5%).
+// 0.608 -> 0.587); RadTan keeps two, direct stores (every setting within
+// 1.5%).  DS: four per lane until its projection's per-point camera
+// constants moved to the host (r05), then two (0.590 -> 0.577 ms,
+// profiles/r05u_ds_ppt.log).
 template <class TagT> struct RoundTripDefault {
     static constexpr int ppt = 1;
     static constexpr bool staged = true;
 };
 template <> struct RoundTripDefault<Tag<DoubleSphere>> {
-    static constexpr int ppt = 4;
+    static constexpr int ppt = 2;
     static constexpr bool staged = true;
 };
 template <> struct RoundTripDefault<Tag<RadTan>> {

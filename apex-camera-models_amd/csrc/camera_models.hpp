@@ -449,7 +449,7 @@ struct RadTan {
     }
     // rad_tan.rs:401-524: Newton on the 2x2 distortion Jacobian, <=100 steps,
     // split into init / step / finish (the round-2 lane-refill experiment ran
-    // the same per-point iterates from them); unproject() chains
+    // the same per-point iterates from them; CHANGELOG round 2); unproject() chains
     // them.
     struct Newton {
         T tx, ty, px, py;
@@ -1109,9 +1109,10 @@ struct DoubleSphere {
         T gamma = xi * d1 + z;
         T d2 = sqrt(r_squared + gamma * gamma);
         T denom = alpha * d2 + (T(1) - alpha) * gamma;
-        // w1, w2 are camera constants (uniform -> scalar unit)
-        T w1 = alpha <= T(0.5) ? alpha / (T(1) - alpha) : (T(1) - alpha) / alpha;
-        T w2 = (w1 + xi) / sqrt(T(2) * w1 * xi + xi * xi + T(1));
+        // w2 (from w1): a camera constant, computed once per camera with the
+        // same IEEE operations (acm.hip unproject_consts, uk[1]; r05: it cost
+        // a division and a square root per point)
+        const T w2 = c.uk[1];
         const bool ok = !(denom < T(1e-3)) && (z > -w2 * d1);
         const T id = FAST ? T(1) / denom : T(0);
         T mx = FAST ? x * id : x / denom, my = FAST ? y * id : y / denom;
@@ -1169,7 +1170,7 @@ struct Ucm {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], alpha = c.p[4];
         T d = sqrt(x * x + y * y + z * z);
         T denom = alpha * d + (T(1) - alpha) * z;
-        T w = alpha <= T(0.5) ? alpha / (T(1) - alpha) : (T(1) - alpha) / alpha;
+        const T w = c.uk[2];  // per camera (acm.hip unproject_consts, r05)
         const bool ok = !(denom < T(1e-3)) && (z > -w * d);
         const T id = FAST ? T(1) / denom : T(0);
         T mx = FAST ? x * id : x / denom, my = FAST ? y * id : y / denom;
@@ -1224,7 +1225,7 @@ struct Eucm {
         T denom = alpha * d + (T(1) - alpha) * z;
         bool cond = true;
         if (alpha > T(0.5)) {
-            T cc = (alpha - T(1)) / (T(2) * alpha - T(1));
+            const T cc = c.uk[1];  // (alpha - 1) / (2 alpha - 1), per camera (r05)
             cond = !(z < denom * cc);
         }
         const bool ok = !(denom < T(1e-3)) && cond;
