@@ -365,8 +365,14 @@ __device__ __forceinline__ void project_point(const Cam<double>& c, size_t n, si
     }
 }
 
+// The per-point projection kernels take CamArg (r05): the per-camera
+// constants of unproject_consts that a projection reads (DS w2, UCM w,
+// EUCM's (alpha - 1) / (2 alpha - 1)) come from the host, computed once with
+// the same IEEE operations, instead of once per lane by make_cam(acm_camera)
+// -- with one point per lane that was once per point (equal speed, measured:
+// profiles/r05aa_residual_camarg.log).
 template <class TagT, int LAYOUT, bool WJ, int VAR>
-__global__ __launch_bounds__(kBlock) void k_project(acm_camera cam, size_t n,
+__global__ __launch_bounds__(kBlock) void k_project(CamArg cam, size_t n,
                                                     const double* __restrict__ pts,
                                                     double* __restrict__ uv,
                                                     uint8_t* __restrict__ status,
@@ -395,7 +401,7 @@ __global__ __launch_bounds__(kBlock) void k_project(acm_camera cam, size_t n,
 // stores.  Not a throughput path (the double-double atan2 costs ~10x the
 // polynomial); the other models are exact in every kernel.
 template <class TagT, int LAYOUT, bool WJ>
-__global__ __launch_bounds__(kBlock) void k_project_exact(acm_camera cam, size_t n,
+__global__ __launch_bounds__(kBlock) void k_project_exact(CamArg cam, size_t n,
                                                           const double* __restrict__ pts,
                                                           double* __restrict__ uv,
                                                           uint8_t* __restrict__ status,
@@ -482,7 +488,7 @@ __device__ __forceinline__ unsigned misalign16(const void* p, size_t elem_offset
 }
 
 template <class TagT, int LAYOUT, bool RESID, bool BASE_AL>
-__global__ __launch_bounds__(kBlock) void k_project_al(acm_camera cam, size_t n,
+__global__ __launch_bounds__(kBlock) void k_project_al(CamArg cam, size_t n,
                                                        const double* __restrict__ pts,
                                                        const double* __restrict__ obs,
                                                        int policy, double* __restrict__ out2,
@@ -511,8 +517,11 @@ __global__ __launch_bounds__(kBlock) void k_project_al(acm_camera cam, size_t n,
         const bool ok = have && st == ST_OK;
         double2 w;
         if (RESID) {
+            // the observations non-temporal (r05): DS at 9.29M 0.247 ->
+            // 0.208 ms, KB -10% (profiles/r05aa_residual_obs_ntl.log); making
+            // the point loads non-temporal too undoes most of it
             double2 o = make_double2(0.0, 0.0);
-            if (have) o = ld2<false>(obs + 2 * p);
+            if (have) o = ld2<true>(obs + 2 * p);
             const double sent = policy == ACM_INVALID_SENTINEL ? 1e6 : 0.0;
             w = make_double2(ok ? u - o.x : sent, ok ? v - o.y : sent);
         } else {
@@ -572,7 +581,7 @@ static bool al_base_aligned(const void* out2, const double* jac) {
 static unsigned al_blocks(size_t n) { return (unsigned)((n + kAlLead - 1 + kAlOwn) / kAlOwn); }
 
 template <class TagT, int LAY, bool RESID>
-static void launch_al(hipStream_t s, const acm_camera& cam, size_t n, const double* pts,
+static void launch_al(hipStream_t s, const CamArg& cam, size_t n, const double* pts,
                       const double* obs, int policy, double* out2, uint8_t* status,
                       double* jac) {
     auto kern = al_base_aligned(out2, jac) ? k_project_al<TagT, LAY, RESID, true>
@@ -770,7 +779,7 @@ template <> struct RoundTripDefault<Tag<Fov>> {  // not measured: as acm_unproje
 
 // -------------------------------------------------- residual + Jacobian
 template <class TagT, int LAYOUT, bool WJ, bool NT>
-__global__ __launch_bounds__(kBlock) void k_residual(acm_camera cam, size_t n,
+__global__ __launch_bounds__(kBlock) void k_residual(CamArg cam, size_t n,
                                                      const double* __restrict__ pts,
                                                      const double* __restrict__ obs,
                                                      int policy, double* __restrict__ res,
@@ -783,7 +792,9 @@ __global__ __launch_bounds__(kBlock) void k_residual(acm_camera cam, size_t n,
     const Cam<double> c = make_cam<double>(cam);
     double x, y, z;
     load_point<LAYOUT>(pts, n, i, x, y, z);
-    const double2 o = *reinterpret_cast<const double2*>(obs + 2 * i);
+    // non-temporal (r05): the residual alone at 9.29M 0.091 -> 0.084 ms
+    // (profiles/r05ab_residual_noj.log)
+    const double2 o = ld2<true>(obs + 2 * i);
     double u, v, ju[P], jv[P];
     const uint8_t st = M::template project<WJ>(c, x, y, z, u, v, ju, jv);
     const bool ok = st == ST_OK;

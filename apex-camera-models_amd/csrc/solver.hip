@@ -293,24 +293,39 @@ ACM_API size_t acm_linear_estimation_with_error_workspace_size(int model, size_t
 }
 
 // One pinned host buffer (R + flag + the 8 statistics) and one event per host
-// thread for the opening's early hand-off, freed when the thread exits.
+// thread for the opening's early hand-off, freed when the thread exits.  The
+// event belongs to the device that was current when it was made: a thread
+// that moves to another device gets a new one.
 namespace {
 struct OpeningHost {
     double* p = nullptr;
     hipEvent_t ev = nullptr;
+    int ev_dev = -1;
     bool ok() {
         if (!p) {
             void* q = nullptr;
-            if (hipHostMalloc(&q, 32 * sizeof(double), hipHostMallocDefault) != hipSuccess) {
+            if (hipHostMalloc(&q, 32 * sizeof(double), hipHostMallocPortable) != hipSuccess) {
                 (void)hipGetLastError();
                 return false;
             }
             p = (double*)q;
         }
-        if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        int dev = -1;
+        if (hipGetDevice(&dev) != hipSuccess) {
             (void)hipGetLastError();
-            ev = nullptr;
             return false;
+        }
+        if (ev && ev_dev != dev) {
+            if (hipEventDestroy(ev) != hipSuccess) (void)hipGetLastError();
+            ev = nullptr;
+        }
+        if (!ev) {
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+                (void)hipGetLastError();
+                ev = nullptr;
+                return false;
+            }
+            ev_dev = dev;
         }
         return true;
     }
