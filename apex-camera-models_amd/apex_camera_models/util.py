@@ -224,15 +224,23 @@ class ValidationResults:
 _REGIONS = (("Center", 0.5), ("Near Center", 0.55), ("Mid Region", 0.65),
             ("Edge Region", 0.8), ("Far Edge", 0.95))
 _VALIDATION_CACHE = {}
+_VALIDATION_CACHE_MAX = 64
 
 
 def _validation_buffers(width: int, height: int):
     """The five test pixels of a resolution, resident on the device, and the
     device / pinned-host result buffers of validate_conversion_accuracy
-    (cached per resolution and device: the call then launches three kernels
-    and copies twice, without building tensors on the host)."""
-    key = (int(width), int(height), torch.cuda.current_device())
+    (cached per resolution, device, stream and thread: the call then launches
+    three kernels and copies twice, without building tensors on the host).
+    Two calls on one device from different threads or streams get different
+    buffers, so neither overwrites the other's results between the copies
+    and the synchronisation; the cache is bounded."""
+    import threading
+    key = (int(width), int(height), torch.cuda.current_device(),
+           torch.cuda.current_stream().cuda_stream, threading.get_ident())
     if key not in _VALIDATION_CACHE:
+        if len(_VALIDATION_CACHE) >= _VALIDATION_CACHE_MAX:
+            _VALIDATION_CACHE.clear()
         w, h = float(width), float(height)
         k = len(_REGIONS)
         pix = torch.tensor([[w * f, h * f] for _, f in _REGIONS], dtype=torch.float64,

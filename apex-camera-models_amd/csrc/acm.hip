@@ -3672,9 +3672,15 @@ static double radtan_newton_disk_uncached(const double* p) {
 }
 
 static double radtan_newton_disk(const double* p) {
+    // a non-finite distortion never gets a disk, and never reaches the memo:
+    // a NaN key would break std::map's ordering
+    for (int i = 4; i < 9; ++i)
+        if (!std::isfinite(p[i])) return 0.0;
     static std::mutex mu;
-    static std::map<std::array<double, 5>, double> memo;
-    const std::array<double, 5> key{p[4], p[5], p[6], p[7], p[8]};
+    // keyed on the bit patterns, so -0.0 and 0.0 are distinct cameras too
+    static std::map<std::array<uint64_t, 5>, double> memo;
+    std::array<uint64_t, 5> key;
+    std::memcpy(key.data(), p + 4, sizeof(key));
     {
         std::lock_guard<std::mutex> lock(mu);
         auto it = memo.find(key);
@@ -3687,7 +3693,13 @@ static double radtan_newton_disk(const double* p) {
     return S;
 }
 
-static CamArg prep(acm_camera c, bool reference_newton = false) {
+// unprojects: the launch's kernels unproject (acm_unproject, the round trip,
+// sample_points, the certificate query).  Only those pay for RadTan's
+// certified disk; every other launch (projection, residuals, the normal
+// equations inside each LM evaluation, statistics, TSQR, undistort) leaves
+// uk[1] = 0 (an LM over RadTan changes the distortion at every
+// step, so the memo missed and each evaluation paid ~ms of host time).
+static CamArg prep(acm_camera c, bool reference_newton = false, bool unprojects = false) {
     if (c.model == ACM_FOV) c.params[8] = std::tan(c.params[4] / 2.0);
     CamArg a;
     static_cast<acm_camera&>(a) = c;
@@ -3700,7 +3712,7 @@ static CamArg prep(acm_camera c, bool reference_newton = false) {
     a.ify = rcp ? recip(c.params[1]) : 0.0;
     unproject_consts<double>(c.model, c.params, a.uk);
 #ifndef ACM_AB_NO_RADTAN_DISK  // A/B build: the per-step tests of r04
-    if (c.model == ACM_RADTAN) a.uk[1] = radtan_newton_disk(c.params);
+    if (c.model == ACM_RADTAN && unprojects) a.uk[1] = radtan_newton_disk(c.params);
 #endif
     if (reference_newton &&
         (c.model == ACM_KANNALA_BRANDT || c.model == ACM_RADTAN || c.model == ACM_FOV))
@@ -4368,7 +4380,7 @@ ACM_API int acm_unproject(const acm_camera* cam, size_t n, const double* points_
                 auto kern = nt ? (ntl ? k_unproject<TagT, L, true, true, K, PR> : k_unproject<TagT, L, true, false, K, PR>)
                                : (ntl ? k_unproject<TagT, L, false, true, K, PR> : k_unproject<TagT, L, false, false, K, PR>);
                 const dim3 gk((unsigned)((n + (size_t)kBlock * K - 1) / ((size_t)kBlock * K)));
-                hipLaunchKernelGGL(kern, gk, b, 0, s, prep(*cam, refn), n, points_2d, rays, status);
+                hipLaunchKernelGGL(kern, gk, b, 0, s, prep(*cam, refn, true), n, points_2d, rays, status);
             };
             using One = std::integral_constant<int, 1>;
             using Two = std::integral_constant<int, 2>;
@@ -4418,7 +4430,7 @@ ACM_API int acm_project_unproject(const acm_camera* cam, size_t n, const double*
             constexpr bool ST = decltype(stg_c)::value && L == ACM_LAYOUT_AOS;
             const dim3 gk((unsigned)((n + (size_t)kBlock * K - 1) / ((size_t)kBlock * K)));
             auto kern = nt ? k_round_trip<TagT, L, true, K, ST> : k_round_trip<TagT, L, false, K, ST>;
-            hipLaunchKernelGGL(kern, gk, b, 0, s, prep(*cam, false), n, points_3d, points_2d,
+            hipLaunchKernelGGL(kern, gk, b, 0, s, prep(*cam, false, true), n, points_3d, points_2d,
                                status, rays, ray_status);
         };
         using AOS = std::integral_constant<int, ACM_LAYOUT_AOS>;
@@ -4767,7 +4779,7 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
     const int pat = g_sample_patience;
     g.patience = pat < 0 ? kLbPatience : pat;
     hipStream_t s = (hipStream_t)stream;
-    CamArg ca = prep(*cam, refn);
+    CamArg ca = prep(*cam, refn, true);
     if (cam->model == ACM_KANNALA_BRANDT && !refn) {
         // the certified kept interval + initial guess for ray_certified, in
         // every sample_points path alike (same rays whichever kernels run)
@@ -4903,7 +4915,7 @@ ACM_API int acm_unproject_certificate(const acm_camera* cam, double* out) {
     if (!out) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
     out[0] = out[1] = 0.0;
     if (cam->model != ACM_RADTAN) return ACM_SUCCESS;
-    const CamArg a = prep(*cam);
+    const CamArg a = prep(*cam, false, true);
     out[0] = a.uk[1];
     out[1] = a.uk[0] == a.uk[0] ? 1.0 : 0.0;
     return ACM_SUCCESS;

@@ -294,14 +294,15 @@ ACM_API size_t acm_linear_estimation_with_error_workspace_size(int model, size_t
 
 // One pinned host buffer (R + flag + the 8 statistics) and one event per host
 // thread for the opening's early hand-off, freed when the thread exits.  The
-// event belongs to the device that was current when it was made: a thread
-// that moves to another device gets a new one.
+// event is made on the device of the caller's stream (which need not be the
+// current one: ADVICE r05), switching to it for the creation only; a stream
+// on another device gets a new event.
 namespace {
 struct OpeningHost {
     double* p = nullptr;
     hipEvent_t ev = nullptr;
     int ev_dev = -1;
-    bool ok() {
+    bool ok(hipStream_t stream) {
         if (!p) {
             void* q = nullptr;
             if (hipHostMalloc(&q, 32 * sizeof(double), hipHostMallocPortable) != hipSuccess) {
@@ -310,21 +311,36 @@ struct OpeningHost {
             }
             p = (double*)q;
         }
-        int dev = -1;
-        if (hipGetDevice(&dev) != hipSuccess) {
+        int cur = -1, dev = -1;
+        if (hipGetDevice(&cur) != hipSuccess) {
             (void)hipGetLastError();
             return false;
+        }
+        dev = cur;
+        if (stream) {
+            hipDevice_t d = 0;
+            if (hipStreamGetDevice(stream, &d) != hipSuccess) {
+                (void)hipGetLastError();
+                return false;
+            }
+            dev = (int)d;
         }
         if (ev && ev_dev != dev) {
             if (hipEventDestroy(ev) != hipSuccess) (void)hipGetLastError();
             ev = nullptr;
         }
         if (!ev) {
-            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            if (dev != cur && hipSetDevice(dev) != hipSuccess) {
                 (void)hipGetLastError();
-                ev = nullptr;
                 return false;
             }
+            const bool made = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+            if (!made) {
+                (void)hipGetLastError();
+                ev = nullptr;
+            }
+            if (dev != cur && hipSetDevice(cur) != hipSuccess) (void)hipGetLastError();
+            if (!made) return false;
             ev_dev = dev;
         }
         return true;
@@ -365,7 +381,7 @@ ACM_API int acm_linear_estimation_with_error_async(acm_camera* cam, size_t n,
                                      workspace_bytes, stream);
     }
     static thread_local OpeningHost host;
-    if (!host.ok()) return sfail(ACM_ERR_HIP, "linear estimation: pinned buffer or event");
+    if (!host.ok(s)) return sfail(ACM_ERR_HIP, "linear estimation: pinned buffer or event");
     const size_t qr = lin_err_qr_bytes(cam->model, n);
     double* d_r = (double*)((char*)workspace + qr);
     int* d_err = (int*)(d_r + 16);
