@@ -66,6 +66,23 @@ class LmSummary(ctypes.Structure):
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                 ctypes.c_void_p)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_size_t, ctypes.c_void_p)
+
+
+class AcmCollective(ctypes.Structure):
+    """acm_collective (include/acm.h, r06): the sharded conversion's
+    stream-ordered all-reduce / all-gather over device f64 buffers."""
+    _fields_ = [
+        ("allreduce", ALLREDUCE_FN),
+        ("allgather", ALLGATHER_FN),
+        ("ctx", ctypes.c_void_p),
+        ("rank", ctypes.c_int32),
+        ("world", ctypes.c_int32),
+    ]
+
+
+RCCL_UNIQUE_ID_BYTES = 128
 TUNE_PROJECT_VARIANT, TUNE_RESIDUAL_NT, TUNE_NE_WAVES, TUNE_FOV_UNROLL, TUNE_NE_UNROLL = 0, 1, 2, 3, 4
 TUNE_ALIGN_J, TUNE_NT_LOADS, TUNE_NT_LOADS_UNPROJECT, TUNE_LM_HOST_RESULT = 5, 6, 7, 8
 TUNE_SAMPLE_FUSED, TUNE_UNPROJECT_RCP, TUNE_SAMPLE_PATIENCE = 9, 10, 11
@@ -127,6 +144,14 @@ EXPORTED_SYMBOLS = (
     "acm_lm_default_config",
     "acm_lm_workspace_size",
     "acm_lm_optimize",
+    "acm_rccl_available",
+    "acm_rccl_unique_id",
+    "acm_rccl_init",
+    "acm_rccl_destroy",
+    "acm_linear_estimation_with_error_sharded_workspace_size",
+    "acm_linear_estimation_with_error_sharded",
+    "acm_reprojection_error_sharded_workspace_size",
+    "acm_reprojection_error_sharded",
     "acm_median_workspace_size",
     "acm_median_valid",
     "acm_median_valid_allreduce",
@@ -268,6 +293,24 @@ def load():
     L.acm_lm_optimize.argtypes = [cam_p, sz, vp, i, vp, ctypes.POINTER(LmConfig), ALLREDUCE_FN,
                                   vp, ctypes.POINTER(LmSummary), vp, sz, vp]
     L.acm_lm_optimize.restype = i
+    coll_p = ctypes.POINTER(AcmCollective)
+    L.acm_rccl_available.argtypes = []
+    L.acm_rccl_available.restype = i
+    L.acm_rccl_unique_id.argtypes = [vp]
+    L.acm_rccl_unique_id.restype = i
+    L.acm_rccl_init.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, coll_p]
+    L.acm_rccl_init.restype = i
+    L.acm_rccl_destroy.argtypes = [coll_p]
+    L.acm_rccl_destroy.restype = i
+    L.acm_linear_estimation_with_error_sharded_workspace_size.argtypes = [i, sz, ctypes.c_int32]
+    L.acm_linear_estimation_with_error_sharded_workspace_size.restype = sz
+    L.acm_linear_estimation_with_error_sharded.argtypes = [cam_p, sz, vp, i, vp, vp, vp, coll_p,
+                                                           vp, sz, vp]
+    L.acm_linear_estimation_with_error_sharded.restype = i
+    L.acm_reprojection_error_sharded_workspace_size.argtypes = [sz, ctypes.c_int32]
+    L.acm_reprojection_error_sharded_workspace_size.restype = sz
+    L.acm_reprojection_error_sharded.argtypes = [cam_p, sz, vp, i, vp, vp, vp, coll_p, vp, sz, vp]
+    L.acm_reprojection_error_sharded.restype = i
     L.acm_median_workspace_size.argtypes = [sz]
     L.acm_median_workspace_size.restype = sz
     L.acm_median_valid.argtypes = [sz, vp, vp, ctypes.c_uint64, vp, vp, sz, vp]

@@ -54,40 +54,31 @@ DISPLAY = {"double_sphere": "Double Sphere", "kannala_brandt": "Kannala-Brandt",
 
 
 def convert(input_model: CameraModel, target: str, points_3d, points_2d,
-            config: LevenbergMarquardtConfig = None, allreduce=None,
-            group=None) -> ConversionMetrics:
+            config: LevenbergMarquardtConfig = None, collective=None) -> ConversionMetrics:
     """One `convert_to_<target>` (e.g. convert_to_double_sphere :355-488).
 
-    Multi-GPU: pass this rank's shard of the correspondences and an
-    `allreduce` hook (distributed.rccl_allreduce(group)); the linear
-    estimation, the LM normal equations and the reprojection statistics then
-    all run over the union of the shards, identically on every rank."""
+    Multi-GPU (r06): pass this rank's shard of the correspondences and a
+    `collective` (distributed.make_collective(group): RCCL driven from libacm
+    under the nccl backend).  The opening (initial error + linear
+    estimation, one fused pass per shard and one all-gather), the LM's
+    normal equations (one all-reduce per evaluation) and the final
+    reprojection error then all run over the union of the shards,
+    identically on every rank, with the same structure as on one GPU."""
     import torch
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     model = _init_target(target, input_model)
-    if allreduce is not None:
-        from . import distributed as D
-        reproj = lambda m: D.distributed_reprojection_error(m, points_3d, points_2d, group)  # noqa: E731
-        estimate = lambda m: D.distributed_linear_estimation(m, points_3d, points_2d, group)  # noqa: E731
-    else:
-        reproj = lambda m: util.compute_reprojection_error(m, points_3d, points_2d)  # noqa: E731
-    finish_initial = None
-    if allreduce is None:
-        # the initial error and the linear estimation in one pass (r04); its
-        # median completes on the stream while the LM starts (r05)
-        initial, finish_initial = util.initial_error_and_linear_estimation(
-            model, points_3d, points_2d, defer_median=True)
-    else:
-        initial = reproj(model)
-        estimate(model)
+    # the initial error and the linear estimation in one pass (r04); its
+    # median completes on the stream while the LM starts (r05)
+    initial, finish_initial = util.initial_error_and_linear_estimation(
+        model, points_3d, points_2d, defer_median=True, collective=collective)
     cfg = config or LevenbergMarquardtConfig()
     status = "Converged"
     res = None
     try:
         res = LevenbergMarquardt(cfg).optimize(model, points_3d, points_2d,
                                                bounds=CONVERTER_BOUNDS[target],
-                                               allreduce=allreduce)
+                                               collective=collective)
         if res.termination == "Failed":
             status = "Linear Only"
     except _lib.AcmError as e:
@@ -100,9 +91,8 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
         status = "Linear Only"
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
-    if finish_initial is not None:
-        initial = finish_initial()
-    final = reproj(model)
+    initial = finish_initial()
+    final = util.compute_reprojection_error(model, points_3d, points_2d, collective=collective)
     # camera_converter.rs:425-438; failed regions come back as NaN (no raise)
     validation = util.validate_conversion_accuracy(model, input_model)
     return ConversionMetrics(model=model, model_name=DISPLAY[target],

@@ -70,6 +70,117 @@ def rccl_allreduce(group=None) -> Callable:
     return cb
 
 
+# ------------------------------------------------------ the collectives
+class TorchCollective:
+    """acm_collective (include/acm.h) whose all-reduce / all-gather are
+    torch.distributed calls on zero-copy views of libacm's device buffers --
+    any backend, including gloo ranks that share one GPU (the tests).  Each
+    collective is a ctypes callback into Python; RcclCollective is the
+    production form with none."""
+
+    def __init__(self, group=None):
+        from . import _lib
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self._views = {}
+
+        def view(ptr, count):
+            key = (int(ptr), int(count))
+            t = self._views.get(key)
+            if t is None:
+                if len(self._views) > 64:
+                    self._views.clear()
+                t = self._views[key] = device_view(int(ptr), int(count))
+            return t
+
+        def allreduce(_ctx, ptr, count, _stream):
+            try:
+                dist.all_reduce(view(ptr, count), op=dist.ReduceOp.SUM, group=group)
+                return 0
+            except Exception:  # noqa: BLE001 -- a failed callback, reported by libacm
+                return -1
+
+        def allgather(_ctx, send, recv, count, _stream):
+            try:
+                r = view(recv, count * self.world)
+                dist.all_gather(list(r.split(int(count))), view(send, count), group=group)
+                return 0
+            except Exception:  # noqa: BLE001
+                return -1
+
+        self._ar = _lib.ALLREDUCE_FN(allreduce)  # kept alive with the struct
+        self._ag = _lib.ALLGATHER_FN(allgather)
+        self.c = _lib.AcmCollective(self._ar, self._ag, None, self.rank, self.world)
+
+    def close(self):
+        self._views.clear()
+
+
+class RcclCollective:
+    """acm_collective over an RCCL communicator that libacm drives itself
+    (acm_rccl_init): rank 0 makes the unique id, torch.distributed
+    broadcasts it once, every rank joins with its own GPU current.  The LM's
+    all-reduce per evaluation and the median's histogram all-reduces are
+    then RCCL calls on the stream from C -- no Python per collective.  One
+    GPU per rank (RCCL refuses two ranks on one device)."""
+
+    def __init__(self, group=None):
+        from . import _lib
+        L = _lib.load()
+        if not L.acm_rccl_available():
+            raise RuntimeError("librccl.so.1 is not loadable: no RCCL collective")
+        if dist.is_available() and dist.is_initialized():
+            self.world = dist.get_world_size(group)
+            self.rank = dist.get_rank(group)
+        else:  # no process group: a 1-rank communicator (bench.py's world-1 leg)
+            self.world, self.rank = 1, 0
+        uid = (ctypes.c_uint8 * _lib.RCCL_UNIQUE_ID_BYTES)()
+        if self.rank == 0:
+            _lib.check(L.acm_rccl_unique_id(uid))
+        obj = [bytes(uid)]
+        if self.world > 1:
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast_object_list(obj, src=src, group=group)
+        uid = (ctypes.c_uint8 * _lib.RCCL_UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
+        self.c = _lib.AcmCollective()
+        _lib.check(L.acm_rccl_init(uid, self.world, self.rank, ctypes.byref(self.c)))
+
+    def close(self):
+        from . import _lib
+        if self.c is not None and self.c.ctx:
+            _lib.check(_lib.load().acm_rccl_destroy(ctypes.byref(self.c)))
+        self.c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
+class LocalCollective:
+    """The 1-rank acm_collective with no callbacks: the sharded entry points
+    then run every merge and the median locally (tests: the sharded path's
+    bits at world 1 without any communicator)."""
+
+    def __init__(self):
+        from . import _lib
+        self.world, self.rank = 1, 0
+        self.c = _lib.AcmCollective(_lib.ALLREDUCE_FN(), _lib.ALLGATHER_FN(), None, 0, 1)
+
+    def close(self):
+        pass
+
+
+def make_collective(group=None):
+    """The sharded conversion's collective for `group`: RcclCollective under
+    the nccl (RCCL) backend with one GPU per rank, else TorchCollective."""
+    if dist.get_backend(group) == "nccl":
+        return RcclCollective(group)
+    return TorchCollective(group)
+
+
 # ------------------------------------------------------- normal equations
 def allreduce_normal_equations(vec: torch.Tensor, group=None) -> torch.Tensor:
     """In-place sum of the packed [JtJ | Jtr | cost | n_valid] vector."""

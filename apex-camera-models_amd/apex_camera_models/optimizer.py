@@ -5,9 +5,9 @@ equations.
 
 `LevenbergMarquardtConfig` keeps apex-solver's builder surface
 (`with_max_iterations`, `with_cost_tolerance`, ...).  For multi-GPU runs pass
-`allreduce=distributed.rccl_allreduce(group)`: each rank holds its shard of
-the correspondences and the (<= 56-double) normal-equation vector is summed
-across ranks before every host solve.
+`collective=distributed.make_collective(group)`: each rank holds its shard of
+the correspondences and the (<= 92-double) normal-equation vector is summed
+across ranks before every host solve (RCCL from C under the nccl backend).
 """
 from __future__ import annotations
 
@@ -85,9 +85,12 @@ class LevenbergMarquardt:
 
     def optimize(self, model: CameraModel, points_3d, points_2d,
                  bounds: Optional[Dict[int, Tuple[float, float]]] = None,
-                 allreduce: Optional[Callable] = None) -> LmResult:
+                 allreduce: Optional[Callable] = None, collective=None) -> LmResult:
         """Optimise model's factor-order parameters in place over the
-        (local shard of the) correspondences."""
+        (local shard of the) correspondences.  collective (r06; e.g.
+        distributed.RcclCollective): its all-reduce sums the normal
+        equations of every evaluation across the ranks, from C; allreduce:
+        a bare Python callback (acm_allreduce_fn) instead."""
         L = _lib.load()
         p3 = _as_device_f64(points_3d, 3)
         p2 = _as_device_f64(points_2d, 2)
@@ -110,9 +113,16 @@ class LevenbergMarquardt:
         ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=p3.device)
         cam = model.acm_camera()
         summ = _lib.LmSummary()
-        cb = _lib.ALLREDUCE_FN(allreduce) if allreduce is not None else _lib.ALLREDUCE_FN()
-        _lib.check(L.acm_lm_optimize(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
-                                     p2.data_ptr(), ctypes.byref(cfg), cb, None,
+        ctx = None
+        if collective is not None:
+            cb, ctx = collective.c.allreduce, collective.c.ctx
+        elif allreduce is not None:
+            cb = _lib.ALLREDUCE_FN(allreduce)
+        else:
+            cb = _lib.ALLREDUCE_FN()
+        _lib.check(L.acm_lm_optimize(ctypes.byref(cam), n, p3.data_ptr() if n else None,
+                                     _lib.LAYOUT_AOS, p2.data_ptr() if n else None,
+                                     ctypes.byref(cfg), cb, ctx,
                                      ctypes.byref(summ), ws.data_ptr(), ws_bytes,
                                      _stream_handle()))
         params = list(cam.params)[: model.NUM_PARAMS]

@@ -81,23 +81,36 @@ def reprojection_stats(camera_model: CameraModel, points3d, points2d, errors=Non
     return out
 
 
-def compute_reprojection_error(camera_model: CameraModel, points3d, points2d) -> ProjectionError:
+def compute_reprojection_error(camera_model: CameraModel, points3d, points2d,
+                               collective=None) -> ProjectionError:
     """error_metrics.rs:62-121: one acm_reprojection_error call (the
     statistics and the median, whose first radix histogram the statistics
-    pass counts) and one device -> host read of its 9 doubles."""
+    pass counts) and one device -> host read of its 9 doubles.
+
+    collective (distributed.RcclCollective / TorchCollective, r06): the
+    points are this rank's shard, and the result is the union's
+    (acm_reprojection_error_sharded), the same on every rank."""
     L = _lib.load()
     p3 = _as_device_f64(points3d, 3)
     p2 = _as_device_f64(points2d, 2)
     n = p3.shape[0]
     if p2.shape[0] != n:
         raise ValueError("points3d and points2d must have the same number of columns")
-    ws_bytes = L.acm_reprojection_error_workspace_size(n)
-    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=p3.device)
     res = torch.empty((9,), dtype=torch.float64, device=p3.device)
     cam = camera_model.acm_camera()
-    _lib.check(L.acm_reprojection_error(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
-                                        p2.data_ptr(), res.data_ptr(), None, ws.data_ptr(),
-                                        ws_bytes, _stream_handle()))
+    if collective is not None:
+        ws_bytes = L.acm_reprojection_error_sharded_workspace_size(n, collective.c.world)
+        ws = _workspace(ws_bytes, p3.device)
+        _lib.check(L.acm_reprojection_error_sharded(
+            ctypes.byref(cam), n, p3.data_ptr() if n else None, _lib.LAYOUT_AOS,
+            p2.data_ptr() if n else None, res.data_ptr(), None, ctypes.byref(collective.c),
+            ws.data_ptr(), ws_bytes, _stream_handle()))
+    else:
+        ws_bytes = L.acm_reprojection_error_workspace_size(n)
+        ws = _workspace(ws_bytes, p3.device)
+        _lib.check(L.acm_reprojection_error(ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS,
+                                            p2.data_ptr(), res.data_ptr(), None, ws.data_ptr(),
+                                            ws_bytes, _stream_handle()))
     out = res.cpu().tolist()
     n_valid = int(out[5])
     if n_valid == 0:
@@ -106,8 +119,12 @@ def compute_reprojection_error(camera_model: CameraModel, points3d, points2d) ->
                            median=out[8], n_valid=n_valid)
 
 
+def _workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(((nbytes + 7) // 8,), dtype=torch.float64, device=device)
+
+
 def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d,
-                                        defer_median: bool = False):
+                                        defer_median: bool = False, collective=None):
     """convert_to_*'s opening (camera_converter.rs:371-375): the reprojection
     error of `model` as given, then `model.linear_estimation` -- for the TSQR
     models one pass over the correspondences (acm_linear_estimation_with_error_async).
@@ -118,24 +135,40 @@ def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d,
     once, `error.median` NaN; the median is still running on the stream and
     finish() returns the completed ProjectionError -- call it after the next
     synchronising step (the LM), so no host round trip separates the opening
-    from the LM's first evaluation."""
+    from the LM's first evaluation.
+
+    collective (r06): the points are this rank's shard and everything is
+    over the union (acm_linear_estimation_with_error_sharded: one all-gather
+    of each rank's factor and statistics, the distributed median); every
+    rank gets the same model."""
     L = _lib.load()
     p3 = _as_device_f64(points3d, 3)
     p2 = _as_device_f64(points2d, 2)
     n = p3.shape[0]
     if p2.shape[0] != n:  # as linear_estimation raises it (kannala_brandt.rs:168-172 & co)
         raise InvalidParams("Number of 2D and 3D points must match")
-    ws_bytes = L.acm_linear_estimation_with_error_workspace_size(model.MODEL_ID, n)
+    if collective is not None:
+        ws_bytes = L.acm_linear_estimation_with_error_sharded_workspace_size(
+            model.MODEL_ID, n, collective.c.world)
+    else:
+        ws_bytes = L.acm_linear_estimation_with_error_workspace_size(model.MODEL_ID, n)
     if ws_bytes == 0:
         raise InvalidParams(f"{model.NAME} has no GPU linear_estimation")
-    ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=p3.device)
+    ws = _workspace(ws_bytes, p3.device)
     # NaN until written: an early error return of the C call leaves it so
     res = torch.full((9,), float("nan"), dtype=torch.float64, device=p3.device)
     host = (ctypes.c_double * 8)(*([float("nan")] * 8))
     cam = model.acm_camera()
-    rc = L.acm_linear_estimation_with_error_async(ctypes.byref(cam), n, p3.data_ptr(),
-                                                  _lib.LAYOUT_AOS, p2.data_ptr(), res.data_ptr(),
-                                                  host, ws.data_ptr(), ws_bytes, _stream_handle())
+    if collective is not None:
+        rc = L.acm_linear_estimation_with_error_sharded(
+            ctypes.byref(cam), n, p3.data_ptr() if n else None, _lib.LAYOUT_AOS,
+            p2.data_ptr() if n else None, res.data_ptr(), host, ctypes.byref(collective.c),
+            ws.data_ptr(), ws_bytes, _stream_handle())
+    else:
+        rc = L.acm_linear_estimation_with_error_async(ctypes.byref(cam), n, p3.data_ptr(),
+                                                      _lib.LAYOUT_AOS, p2.data_ptr(),
+                                                      res.data_ptr(), host, ws.data_ptr(),
+                                                      ws_bytes, _stream_handle())
     if rc not in (_lib.ACM_SUCCESS, _lib.ERR_INVALID_PARAMS, _lib.ERR_NUMERICAL):
         _lib.check(rc)
     out = list(host)

@@ -5052,10 +5052,13 @@ namespace acm {
 // right after the statistics -- before the median -- R and the flag (17 f64
 // from r_factor, the flag in r_factor[16]) and result[0..7] are copied there
 // and `ready` is recorded, so the host can solve while the median runs.
+// hist_nb != nullptr (the sharded opening, sharded.hip): the shard's R, flag
+// and 8 statistics only -- no median state, no host copy, no median; the
+// pass-0 histogram partials stay in ws_err and *hist_nb = their workgroups.
 int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                            const double* points_2d, double* r_factor, int* error_flag,
                            double* result, void* ws_qr, void* ws_err, void* stream,
-                           double* host_out, hipEvent_t ready) {
+                           double* host_out, hipEvent_t ready, int* hist_nb) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -5094,8 +5097,12 @@ int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points
     }
     void* mws = (char*)ws_err + reproj_error_median_offset(n);
     hipLaunchKernelGGL(k_reproj_finish, dim3(1), dim3(kBlock), 0, s, p1, nb, tot, result,
-                       sel_ws(mws));
+                       hist_nb ? SelWs{} : sel_ws(mws));
     if ((rc = check_launch("acm_linear_estimation_with_error"))) return rc;
+    if (hist_nb) {
+        *hist_nb = nb;
+        return ACM_SUCCESS;
+    }
     if (host_out) {
         if (hipMemcpyAsync(host_out, r_factor, 17 * sizeof(double), hipMemcpyDeviceToHost, s) !=
                 hipSuccess ||
@@ -5106,6 +5113,27 @@ int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points
     }
     return median_impl(n, errs, result + 5, 0, result + 8, mws, nullptr, nullptr, stream, hparts,
                        nb, true);
+}
+
+// The sharded conversion's pieces (sharded.hip): the workspace layout of
+// acm_reprojection_error, its statistics pass with the pass-0 histogram
+// partials but no median state, and the median of the union of the ranks'
+// values for a global n_valid known on the host, every histogram summed
+// through `allreduce`.
+size_t reproj_error_hist_off(size_t n) { return reproj_error_hist_offset(n); }
+size_t reproj_error_median_off(size_t n) { return reproj_error_median_offset(n); }
+int reprojection_stats_hist(const acm_camera* cam, size_t n, const double* points_3d, int layout,
+                            const double* points_2d, double* result, double* errors,
+                            void* workspace, void* stream, int* hist_nb) {
+    unsigned int* hparts = (unsigned int*)((char*)workspace + reproj_error_hist_offset(n));
+    return reprojection_stats_impl(cam, n, points_3d, layout, points_2d, result, errors,
+                                   workspace, (hipStream_t)stream, hparts, hist_nb);
+}
+int median_union(size_t n, const double* values, uint64_t n_valid_global, double* out,
+                 void* median_ws, acm_allreduce_fn allreduce, void* allreduce_ctx, void* stream,
+                 const unsigned int* hparts, int hist_nb) {
+    return median_impl(n, values, nullptr, n_valid_global, out, median_ws, allreduce,
+                       allreduce_ctx, stream, hparts, hist_nb, false);
 }
 }  // namespace acm
 }

@@ -33,7 +33,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
 int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                            const double* points_2d, double* r_factor, int* error_flag,
                            double* result, void* ws_qr, void* ws_err, void* stream,
-                           double* host_out, hipEvent_t ready);
+                           double* host_out, hipEvent_t ready, int* hist_nb = nullptr);
 }
 
 namespace {
@@ -416,6 +416,18 @@ ACM_API int acm_linear_estimation_with_error(acm_camera* cam, size_t n, const do
     return rc;
 }
 
+// (r06) after the all-reduce: the R summed results into the pinned buffer,
+// then the completion word with a system-scope release (one lane: R <= 92)
+__global__ void k_lm_copy_publish(const double* __restrict__ src, double* __restrict__ dst,
+                                  int count, unsigned long long* __restrict__ flag,
+                                  unsigned long long seq) {
+    if (threadIdx.x == 0) {
+        for (int t = 0; t < count; ++t) dst[t] = src[t];
+        __threadfence_system();
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 ACM_API void acm_lm_default_config(acm_lm_config* cfg) {
     if (!cfg) return;
     std::memset(cfg, 0, sizeof(*cfg));
@@ -472,10 +484,13 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
     static thread_local PinnedResults tl;
     double*& pinned = tl.p;
     unsigned long long& seq = tl.seq;
-    const int host_mode = allreduce ? 0 : acm::lm_host_result();
-    double* res_out = d_res;
-    unsigned long long* flag = nullptr;
-    if (!allreduce && !pinned) {
+    // (r06) With an all-reduce the epilogue writes device memory, the
+    // callback sums it in place on the stream (RCCL), and in mode 2 one
+    // single-lane kernel then copies the sums into the pinned buffer and
+    // publishes the completion word: the host spins as without an
+    // all-reduce, instead of a pageable copy and a stream synchronisation.
+    const int knob = acm::lm_host_result();
+    if (knob && !pinned) {
         void* p = nullptr;
         if (hipHostMalloc(&p, 128 * sizeof(double),
                           hipHostMallocMapped | hipHostMallocPortable |
@@ -484,13 +499,17 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
         else
             (void)hipGetLastError();
     }
-    // the finish kernel's ticket (mode 2): one of d_res's spare words, zeroed
-    // here and re-armed by the last workgroup of every evaluation
+    const int host_mode = pinned ? knob : 0;
+    double* res_out = d_res;
+    unsigned long long* flag = nullptr;
+    // the finish kernel's ticket (mode 2 without an all-reduce): one of
+    // d_res's spare words, zeroed here and re-armed by the last workgroup of
+    // every evaluation
     unsigned int* ticket = nullptr;
-    if (host_mode && pinned) {
+    if (host_mode == 2) flag = reinterpret_cast<unsigned long long*>(pinned + 127);
+    if (host_mode && !allreduce) {
         res_out = pinned;
         if (host_mode == 2) {
-            flag = reinterpret_cast<unsigned long long*>(pinned + 127);
             ticket = reinterpret_cast<unsigned int*>(d_res + R);
             if (hip_ok(hipMemsetAsync(ticket, 0, sizeof(unsigned int), s)))
                 return sfail(ACM_ERR_HIP, "LM: ticket reset failed");
@@ -504,11 +523,20 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
         const unsigned long long want = flag ? ++seq : 0;
         int rc = acm::normal_equations_impl(&c, n, points_3d, layout, points_2d,
                                             cfg->invalid_policy, res_out, workspace, ne_ws, stream,
-                                            flag, want, ticket);
+                                            allreduce ? nullptr : flag, want, ticket);
         if (rc) return rc;
         if (allreduce) {
             rc = allreduce(allreduce_ctx, d_res, (size_t)R, stream);
             if (rc) return sfail(ACM_ERR_HIP, "all-reduce callback failed");
+            if (flag) {
+                hipLaunchKernelGGL(k_lm_copy_publish, dim3(1), dim3(64), 0, s, d_res, pinned, R,
+                                   flag, want);
+                if (hip_ok(hipGetLastError())) return sfail(ACM_ERR_HIP, "LM: publish launch");
+            } else if (host_mode == 1 &&
+                       hip_ok(hipMemcpyAsync(pinned, d_res, R * sizeof(double),
+                                             hipMemcpyDeviceToHost, s))) {
+                return sfail(ACM_ERR_HIP, "LM: device copy failed");
+            }
         }
         if (flag) {
             // spin on the completion word; every 256 polls ask the stream, so
@@ -525,10 +553,10 @@ ACM_API int acm_lm_optimize(acm_camera* cam, size_t n, const double* points_3d, 
                 }
                 __builtin_ia32_pause();
             }
-            std::memcpy(out, res_out, R * sizeof(double));
-        } else if (res_out != d_res) {
+            std::memcpy(out, pinned, R * sizeof(double));
+        } else if (host_mode == 1) {
             if (hip_ok(hipStreamSynchronize(s))) return sfail(ACM_ERR_HIP, "LM: stream failed");
-            std::memcpy(out, res_out, R * sizeof(double));
+            std::memcpy(out, pinned, R * sizeof(double));
         } else if (hip_ok(hipMemcpyAsync(out, d_res, R * sizeof(double), hipMemcpyDeviceToHost,
                                          s)) ||
                    hip_ok(hipStreamSynchronize(s))) {

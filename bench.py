@@ -568,17 +568,48 @@ def leg_config5(ctx, n_cells):
     uv, xyz, total = sample()
     ctx.sync()
     t_s = ctx.max_over_ranks(time.perf_counter() - t0)
-    allreduce = D.rccl_allreduce() if ctx.dist else None
-    # one untimed conversion first (its multi-GB workspaces' first
-    # allocation), then the fastest of three, each the max over ranks
-    conversion.convert(src, "double_sphere", xyz, uv, allreduce=allreduce)
-    t_c, met = float("inf"), None
-    for _ in range(3):
-        ctx.sync()
-        t0 = time.perf_counter()
-        met = conversion.convert(src, "double_sphere", xyz, uv, allreduce=allreduce)
-        ctx.sync()
-        t_c = min(t_c, ctx.max_over_ranks(time.perf_counter() - t0))
+    # N > 1: the sharded conversion over RCCL driven from libacm (r06; gloo
+    # rehearsals: torch.distributed callbacks).  N = 1: the 1-GPU path, and
+    # beside it the same sharded path under a 1-rank RCCL communicator
+    # (its overhead on one GPU, and the same bits).
+    coll = D.make_collective() if ctx.dist else None
+    sharded1 = None
+    if not ctx.dist:
+        try:
+            sharded1 = D.RcclCollective()
+        except Exception as e:  # noqa: BLE001 -- reported in the line, headline kept
+            sharded1 = f"{type(e).__name__}: {e}"[:200]
+
+    def timed(c):
+        # one untimed conversion first (its multi-GB workspaces' first
+        # allocation), then the fastest of three, each the max over ranks
+        conversion.convert(src, "double_sphere", xyz, uv, collective=c)
+        t, m = float("inf"), None
+        for _ in range(3):
+            ctx.sync()
+            t0 = time.perf_counter()
+            m = conversion.convert(src, "double_sphere", xyz, uv, collective=c)
+            ctx.sync()
+            t = min(t, ctx.max_over_ranks(time.perf_counter() - t0))
+        return t, m
+
+    t_c, met = timed(coll)
+    world1 = None
+    if isinstance(sharded1, str):
+        world1 = {"error": sharded1}
+    elif sharded1 is not None:
+        t1, m1 = timed(sharded1)
+        world1 = {"what": "the sharded conversion (acm_*_sharded + RCCL from libacm) under a "
+                          "1-rank communicator on this GPU",
+                  "convert_ms": round(t1 * 1e3, 3),
+                  "over_1gpu_path_pct": round(100 * (t1 / t_c - 1), 2),
+                  "same_bits": (m1.model.params() == met.model.params()
+                                and m1.final_reprojection_error.median ==
+                                met.final_reprojection_error.median
+                                and m1.initial_reprojection_error.median ==
+                                met.initial_reprojection_error.median
+                                and m1.lm_iterations == met.lm_iterations)}
+        sharded1.close()
     out = {"what": "KB->DS conversion: sharded sample_points + linear estimation + bounded LM "
                    "+ reprojection errors",
            "requested_cells": n_cells, "grid": [ncx, ncy], "correspondences_total": total,
@@ -589,6 +620,12 @@ def leg_config5(ctx, n_cells):
            "final_mean_px": met.final_reprojection_error.mean,
            "final_median_px": met.final_reprojection_error.median,
            "ds_params": met.model.params(), "scaling": "strong"}
+    if ctx.dist:
+        out["collective"] = type(coll).__name__
+        if hasattr(coll, "close"):
+            coll.close()
+    if world1 is not None:
+        out["sharded_world1"] = world1
     del uv, xyz
     torch.cuda.empty_cache()
     return out

@@ -382,6 +382,73 @@ ACM_API int acm_lm_optimize(acm_camera *cam, size_t n, const double *points_3d,
                             void *allreduce_ctx, acm_lm_summary *summary,
                             void *workspace, size_t workspace_bytes, void *stream);
 
+/* (r06) The sharded conversion's collectives.  One
+ * process per GPU, each holding a shard of the correspondences; both
+ * collectives are stream-ordered on device f64 buffers:
+ *   allreduce -- in-place sum over the ranks (the acm_allreduce_fn of
+ *                acm_lm_optimize / acm_median_valid_allreduce);
+ *   allgather -- every rank's `count` values into recv (world x count, in
+ *                rank order).
+ * acm_rccl_init builds one over an RCCL communicator that libacm drives
+ * itself (librccl.so.1: the copy already loaded in the process, e.g.
+ * torch's, else ROCm's), so no Python runs per collective; rank 0 makes the
+ * id (acm_rccl_unique_id), the caller broadcasts it (e.g. through
+ * torch.distributed) and every rank calls acm_rccl_init with its own GPU
+ * current -- one GPU per rank.  acm_rccl_destroy frees it.  Any other
+ * transport can fill the struct with its own callbacks (the tests' gloo
+ * ranks sharing one GPU do). */
+typedef int (*acm_allgather_fn)(void *ctx, const double *send, double *recv,
+                                size_t count, void *stream);
+typedef struct acm_collective {
+    acm_allreduce_fn allreduce;
+    acm_allgather_fn allgather;
+    void *ctx;
+    int32_t rank;
+    int32_t world;
+} acm_collective;
+#define ACM_RCCL_UNIQUE_ID_BYTES 128
+ACM_API int acm_rccl_available(void);
+ACM_API int acm_rccl_unique_id(uint8_t *id);
+ACM_API int acm_rccl_init(const uint8_t *id, int32_t world, int32_t rank,
+                          acm_collective *out);
+ACM_API int acm_rccl_destroy(acm_collective *coll);
+
+/* (r06) convert_to_*'s opening over the union of the ranks' shards
+ * (camera_converter.rs:371-375; the multi-GPU form of
+ * acm_linear_estimation_with_error_async): per shard the same fused pass
+ * (R factor, error flag, the 8 statistics, the median's first histogram),
+ * then ONE all-gather of a 32-double record per rank, the rank-ordered
+ * Givens merge of the factors and Chan merge of the statistics on the host,
+ * the exact median of the union (every histogram summed by coll->allreduce;
+ * it lands in initial_error[8] in stream order, initial_error[0..7] hold the
+ * union's statistics), and the solve (count checks on the union's size).
+ * FOV: the statistics, then the grid sums all-reduced and
+ * acm_fov_grid_select.  Every rank gets the same cam->params bit for bit;
+ * with one rank (coll NULL, or world 1) the bits of the 1-GPU call.
+ * initial_error_host: nullable, host, the union's 8 statistics. */
+ACM_API size_t acm_linear_estimation_with_error_sharded_workspace_size(int model, size_t n,
+                                                                       int32_t world);
+ACM_API int acm_linear_estimation_with_error_sharded(acm_camera *cam, size_t n,
+                                                     const double *points_3d, int layout,
+                                                     const double *points_2d,
+                                                     double *initial_error,
+                                                     double *initial_error_host,
+                                                     const acm_collective *coll,
+                                                     void *workspace, size_t workspace_bytes,
+                                                     void *stream);
+/* (r06) compute_reprojection_error (error_metrics.rs:62-121) over the union
+ * of the ranks' shards: this shard's statistics pass (with the median's
+ * first histogram), one all-gather of the records, Chan's merge, the
+ * distributed exact median.  result: device, 9 f64 as acm_reprojection_error
+ * (the union's), identical on every rank; errors: nullable device N f64. */
+ACM_API size_t acm_reprojection_error_sharded_workspace_size(size_t n, int32_t world);
+ACM_API int acm_reprojection_error_sharded(const acm_camera *cam, size_t n,
+                                           const double *points_3d, int layout,
+                                           const double *points_2d, double *result,
+                                           double *errors, const acm_collective *coll,
+                                           void *workspace, size_t workspace_bytes,
+                                           void *stream);
+
 /* Exact median of the non-NaN values of `values` (the per-point errors of
  * acm_reprojection_stats), error_metrics.rs:103-111: the mean of ranks
  * m/2-1 and m/2 for even m, rank m/2 for odd m, m = n_valid (read from

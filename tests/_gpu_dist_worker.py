@@ -78,13 +78,15 @@ def main():
     src = KannalaBrandtModel._from_params(kp, Resolution(kw, kh))
     uv_all, xyz_all = util.sample_points(src, 4000)
     slo, shi = D.shard_range(uv_all.shape[0], rank, world)
+    coll = D.TorchCollective()  # gloo ranks share the box's one GPU (RCCL needs one each)
     for tgt in ("double_sphere", "kannala_brandt", "rad_tan", "fov"):
-        met = conversion.convert(src, tgt, xyz_all[slo:shi], uv_all[slo:shi],
-                                 allreduce=D.rccl_allreduce())
+        met = conversion.convert(src, tgt, xyz_all[slo:shi], uv_all[slo:shi], collective=coll)
         out[f"lm_params_{tgt}"] = np.array(met.model.params())
         out[f"lm_iters_{tgt}"] = np.array([met.lm_iterations])
         fe = met.final_reprojection_error
         out[f"lm_err_{tgt}"] = np.array([fe.mean, fe.median, fe.n_valid])
+        ie = met.initial_reprojection_error
+        out[f"init_err_{tgt}"] = np.array([ie.mean, ie.median, ie.n_valid, ie.min, ie.max])
     np.savez(os.path.join(a.out, f"rank{rank}.npz"), **out)
     dist.barrier()
     dist.destroy_process_group()

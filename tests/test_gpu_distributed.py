@@ -87,6 +87,15 @@ def test_sharded_gpu_path_matches_single_process(world, tmp_path):
         for r in res:
             assert np.array_equal(r[f"lm_params_{tgt}"], p0)  # ranks agree bit for bit
         np.testing.assert_allclose(p0, ref.model.params(), rtol=1e-8, atol=1e-10)
+        # the initial error of the sharded opening (one fused pass per
+        # shard, one all-gather, the distributed median) == the 1-GPU one:
+        # count, extrema and median exact, the mean to rounding
+        for r in res:
+            ie = r[f"init_err_{tgt}"]
+            ri = ref.initial_reprojection_error
+            assert ie[2] == ri.n_valid and ie[1] == ri.median
+            assert ie[3] == ri.min and ie[4] == ri.max
+            assert abs(ie[0] - ri.mean) <= 1e-12 * ri.mean
         fe = res[0][f"lm_err_{tgt}"]
         assert fe[2] == ref.final_reprojection_error.n_valid
         # the sharded sums round differently (~1e-16 relative); RadTan fitted

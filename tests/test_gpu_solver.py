@@ -178,7 +178,9 @@ def test_lm_rccl_allreduce_single_rank():
 
     import torch.distributed as dist
     from apex_camera_models import KannalaBrandtModel, Resolution, conversion, util
+    from apex_camera_models import distributed as D
     from apex_camera_models.distributed import rccl_allreduce
+    from apex_camera_models.optimizer import CONVERTER_BOUNDS, LevenbergMarquardt
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -189,9 +191,17 @@ def test_lm_rccl_allreduce_single_rank():
         src = KannalaBrandtModel._from_params(params, Resolution(w, h))
         uv, xyz = util.sample_points(src, 500)
         a = conversion.convert(src, "double_sphere", xyz, uv)
-        b = conversion.convert(src, "double_sphere", xyz, uv, allreduce=rccl_allreduce())
-        assert a.model.params() == b.model.params()
-        assert a.lm_iterations == b.lm_iterations
+        b = LevenbergMarquardt().optimize(
+            conversion._init_target("double_sphere", src), xyz, uv,
+            bounds=CONVERTER_BOUNDS["double_sphere"], allreduce=rccl_allreduce())
+        c = LevenbergMarquardt().optimize(
+            conversion._init_target("double_sphere", src), xyz, uv,
+            bounds=CONVERTER_BOUNDS["double_sphere"])
+        assert b.parameters == c.parameters and b.iterations == c.iterations
+        d = conversion.convert(src, "double_sphere", xyz, uv,
+                               collective=D.TorchCollective())
+        assert a.model.params() == d.model.params()
+        assert a.lm_iterations == d.lm_iterations
     finally:
         dist.destroy_process_group()
 
