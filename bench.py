@@ -49,6 +49,31 @@ BYTES_PER_POINT = {  # algorithmic bytes / point for project (+J), SURVEY.md §8
     ("kb", True): 24 + 16 + 1 + 16 * 8, ("kb", False): 24 + 16 + 1,
 }
 MODELS = {"pinhole": 0, "radtan": 1, "kb": 2, "ds": 3, "ucm": 4, "eucm": 5, "fov": 6}
+IC_BYTES = 256 << 20  # MI355X Infinity Cache (MI355X_MICROARCH.md)
+RT_BYTES_PER_POINT = 24 + 16 + 1 + 24 + 1  # config 4's one-pass round trip
+
+
+def roofline_block(bytes_per_launch, input_bytes_per_launch, kernel_ms):
+    """Roofline of a sub-measurement: algorithmic bytes
+    per launch / its time against the HBM peak.  When everything a launch
+    touches fits the 256 MiB Infinity Cache (the strong-scaling shards at
+    N = 8: 1.25M KB points, 211 MB), back-to-back launches are served partly
+    from it: bound "effective (Infinity Cache)", not "hbm".  When only the
+    re-read inputs fit (config 4's 6.25M-point shards at N = 8: 150 MB of
+    input, 412 MB in all) the bound stays "hbm" and input_fits_infinity_cache
+    says the reads may be cache-assisted."""
+    ic = bytes_per_launch < IC_BYTES
+    out = {"bound": "effective (Infinity Cache)" if ic else "hbm",
+           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "algorithmic_bytes_per_launch": int(bytes_per_launch),
+           "input_bytes_per_launch": int(input_bytes_per_launch),
+           "input_fits_infinity_cache": bool(input_bytes_per_launch < IC_BYTES),
+           "achieved": None, "frac": None, "kernel_ms": kernel_ms}
+    if kernel_ms:
+        a = bytes_per_launch / (kernel_ms / 1e3) / 1e9
+        out["achieved"] = round(a, 1)
+        out["frac"] = round(a / HBM_PEAK_GBS, 4)
+    return out
 
 
 def parse():
@@ -518,6 +543,7 @@ def leg_config4(ctx, n_total, reps):
     for k, name in enumerate(LEG4_MODELS.values()):
         models[name] = {"round_trip_ms": round(per_model[k], 4),
                         "Mpoints_per_s": round(n_total / per_model[k] / 1e3, 1),
+                        "roofline": roofline_block(RT_BYTES_PER_POINT * n, 24 * n, per_model[k]),
                         "round_trip_ok": int(vec[2 * k + 1]),
                         "rms_round_trip_err": (vec[2 * k] / vec[2 * k + 1]) ** 0.5
                         if vec[2 * k + 1] else None}
@@ -692,8 +718,17 @@ def main():
     if rehearsal:
         wd.disarm()
         if rank == 0:
+            # the labels the GPU run would attach for these shard sizes
+            from apex_camera_models.distributed import shard_range
+            bpp = 24 + 16 + 1 + (16 * 8 if not a.no_jacobian else 0)
+            n_strong = shard_range(a.points, 0, world)[1]
+            n4 = shard_range(a.leg4_points, 0, world)[1]
+            planned = {"weak": roofline_block(bpp * a.points, 24 * a.points, None)["bound"],
+                       "strong": roofline_block(bpp * n_strong, 24 * n_strong, None)["bound"],
+                       "config4": roofline_block(RT_BYTES_PER_POINT * n4, 24 * n4, None)["bound"]}
             print(json.dumps({"rehearsal": "cpu", "n_ranks_seen": world,
-                              "ranks_devices": ranks_devices}), flush=True)
+                              "ranks_devices": ranks_devices, "planned_bounds": planned}),
+                  flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -921,6 +956,8 @@ def main():
         if "shards_match_single_projection" in main_res:
             out["shards_match_single_projection"] = main_res["shards_match_single_projection"]
         if other is not None:
+            npr = other["points_per_rank"]
+            other["roofline"] = roofline_block(bpp * npr, 24 * npr, other["kernel_ms"])
             out[other["mode"]] = other
         out.update(legs)
         wd.arm("cpu baseline", 10 * tmo)

@@ -180,6 +180,38 @@ def test_cpu_rehearsal_device_census_world2():
     assert [(x["rank"], x["local_rank"]) for x in d["ranks_devices"]] == [(0, 0), (1, 1)]
 
 
+def test_cpu_rehearsal_labels_infinity_cache_shards_world2():
+    """at world 2 with a small strong batch (2M KB
+    points: 1M per rank, 169 MB with the Jacobian) and config 4's shards
+    (1M points per rank, 66 MB) everything a launch touches fits the
+    256 MiB Infinity Cache, and the line's planned bounds say "effective
+    (Infinity Cache)"; the weak shard (2M points per rank, 338 MB) stays
+    "hbm"."""
+    import json
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--points", "2000000",
+                        "--leg4-points", "2000000"],
+                       env=_env(ACM_BENCH_BACKEND="gloo", ACM_BENCH_CPU_REHEARSAL="1",
+                                ACM_BENCH_TIMEOUT="60"),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["planned_bounds"] == {"weak": "hbm", "strong": "effective (Infinity Cache)",
+                                   "config4": "effective (Infinity Cache)"}
+
+
+def test_roofline_block_rule():
+    import bench
+    big = bench.roofline_block(169 * 10_000_000, 24 * 10_000_000, 0.25)
+    assert big["bound"] == "hbm" and abs(big["frac"] - 0.845) < 1e-9
+    # N = 8 strong shard: 1.25M KB points, 211 MB in all
+    assert bench.roofline_block(169 * 1_250_000, 24 * 1_250_000, 0.03)["bound"] == \
+        "effective (Infinity Cache)"
+    # config 4 at N = 8: 6.25M points, 412 MB in all but 150 MB of re-read input
+    c4 = bench.roofline_block(66 * 6_250_000, 24 * 6_250_000, None)
+    assert c4["bound"] == "hbm" and c4["input_fits_infinity_cache"]
+    assert bench.roofline_block(66 * 50_000_000, 24 * 50_000_000, 0.6)["bound"] == "hbm"
+
+
 def test_withheld_collective_exits_within_bound():
     """one rank never joins the first collective; the job
     ends non-zero within the bound (ACM_BENCH_TIMEOUT = 5 s, not the
