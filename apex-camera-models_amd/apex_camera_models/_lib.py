@@ -83,6 +83,16 @@ class AcmCollective(ctypes.Structure):
 
 
 RCCL_UNIQUE_ID_BYTES = 128
+
+
+class CellGrid(ctypes.Structure):
+    """acm_cell_grid (include/acm.h, r06): the grid of a cell-form sample."""
+    _fields_ = [
+        ("num_cells_x", ctypes.c_uint32),
+        ("num_cells_y", ctypes.c_uint32),
+        ("width", ctypes.c_uint32),
+        ("height", ctypes.c_uint32),
+    ]
 TUNE_PROJECT_VARIANT, TUNE_RESIDUAL_NT, TUNE_NE_WAVES, TUNE_FOV_UNROLL, TUNE_NE_UNROLL = 0, 1, 2, 3, 4
 TUNE_ALIGN_J, TUNE_NT_LOADS, TUNE_NT_LOADS_UNPROJECT, TUNE_LM_HOST_RESULT = 5, 6, 7, 8
 TUNE_SAMPLE_FUSED, TUNE_UNPROJECT_RCP, TUNE_SAMPLE_PATIENCE = 9, 10, 11
@@ -144,6 +154,9 @@ EXPORTED_SYMBOLS = (
     "acm_lm_default_config",
     "acm_lm_workspace_size",
     "acm_lm_optimize",
+    "acm_normal_equations_cells",
+    "acm_lm_optimize_cells",
+    "acm_sample_points_cells",
     "acm_rccl_available",
     "acm_rccl_unique_id",
     "acm_rccl_init",
@@ -293,6 +306,14 @@ def load():
     L.acm_lm_optimize.argtypes = [cam_p, sz, vp, i, vp, ctypes.POINTER(LmConfig), ALLREDUCE_FN,
                                   vp, ctypes.POINTER(LmSummary), vp, sz, vp]
     L.acm_lm_optimize.restype = i
+    grid_p = ctypes.POINTER(CellGrid)
+    L.acm_normal_equations_cells.argtypes = [cam_p, sz, vp, i, vp, grid_p, i, vp, vp, sz, vp]
+    L.acm_normal_equations_cells.restype = i
+    L.acm_lm_optimize_cells.argtypes = [cam_p, sz, vp, i, vp, grid_p, ctypes.POINTER(LmConfig),
+                                        ALLREDUCE_FN, vp, ctypes.POINTER(LmSummary), vp, sz, vp]
+    L.acm_lm_optimize_cells.restype = i
+    L.acm_sample_points_cells.argtypes = [cam_p, sz, sz, sz, i, vp, vp, vp, vp, vp, sz, vp]
+    L.acm_sample_points_cells.restype = i
     coll_p = ctypes.POINTER(AcmCollective)
     L.acm_rccl_available.argtypes = []
     L.acm_rccl_available.restype = i

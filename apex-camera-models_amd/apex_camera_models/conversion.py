@@ -54,7 +54,8 @@ DISPLAY = {"double_sphere": "Double Sphere", "kannala_brandt": "Kannala-Brandt",
 
 
 def convert(input_model: CameraModel, target: str, points_3d, points_2d,
-            config: LevenbergMarquardtConfig = None, collective=None) -> ConversionMetrics:
+            config: LevenbergMarquardtConfig = None, collective=None,
+            cells=None) -> ConversionMetrics:
     """One `convert_to_<target>` (e.g. convert_to_double_sphere :355-488).
 
     Multi-GPU (r06): pass this rank's shard of the correspondences and a
@@ -63,7 +64,11 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
     estimation, one fused pass per shard and one all-gather), the LM's
     normal equations (one all-reduce per evaluation) and the final
     reprojection error then all run over the union of the shards,
-    identically on every rank, with the same structure as on one GPU."""
+    identically on every rank, with the same structure as on one GPU.
+
+    cells (r06): the util.CellSample of points_2d when the correspondences
+    come from sample_points(..., cells=True): the LM's evaluations read the
+    4-B cells instead of the 16-B pixels, with the same iterates."""
     import torch
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -78,7 +83,7 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
     try:
         res = LevenbergMarquardt(cfg).optimize(model, points_3d, points_2d,
                                                bounds=CONVERTER_BOUNDS[target],
-                                               collective=collective)
+                                               collective=collective, cells=cells)
         if res.termination == "Failed":
             status = "Linear Only"
     except _lib.AcmError as e:

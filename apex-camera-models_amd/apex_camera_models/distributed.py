@@ -407,20 +407,27 @@ def sharded_sample_points(ncx: int, ncy: int, rank: int, world: int,
     rank's grid rows; return (uv, xyz, global_offset, global_total) so that
     the rank-ordered concatenation equals the serial sample_points output."""
     c0, c1 = grid_row_range(ncx, ncy, rank, world)
-    uv, xyz = local_fn(c0, c1)
+    out = local_fn(c0, c1)
+    uv = out[0]
     m = torch.tensor([uv.shape[0]], dtype=torch.int64, device=uv.device)
     counts = [torch.zeros_like(m) for _ in range(world)]
     dist.all_gather(counts, m, group=group)
     counts = [int(c) for c in counts]
-    return uv, xyz, sum(counts[:rank]), sum(counts)
+    return (*out, sum(counts[:rank]), sum(counts))
 
 
-def gpu_sample_points_range(model, n_requested: int):
-    """local_fn for sharded_sample_points backed by acm_sample_points_range."""
+def gpu_sample_points_range(model, n_requested: int, cells: bool = False):
+    """local_fn for sharded_sample_points backed by acm_sample_points_range
+    (cells=True: util.sample_points' cell form, (uv, xyz, CellSample) with
+    the global cell ids of the shard's rows)."""
     from . import _lib
     from .camera import _stream_handle
     L = _lib.load()
     cam = model.acm_camera()
+    if cells:
+        from . import util
+        return lambda c0, c1: util.sample_points(model, n_requested, cells=True,
+                                                 cell_range=(c0, c1))
 
     def fn(c0, c1):
         cells = max(c1 - c0, 0)

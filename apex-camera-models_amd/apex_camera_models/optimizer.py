@@ -85,12 +85,16 @@ class LevenbergMarquardt:
 
     def optimize(self, model: CameraModel, points_3d, points_2d,
                  bounds: Optional[Dict[int, Tuple[float, float]]] = None,
-                 allreduce: Optional[Callable] = None, collective=None) -> LmResult:
+                 allreduce: Optional[Callable] = None, collective=None,
+                 cells=None) -> LmResult:
         """Optimise model's factor-order parameters in place over the
         (local shard of the) correspondences.  collective (r06; e.g.
         distributed.RcclCollective): its all-reduce sums the normal
         equations of every evaluation across the ranks, from C; allreduce:
-        a bare Python callback (acm_allreduce_fn) instead."""
+        a bare Python callback (acm_allreduce_fn) instead.  cells (r06):
+        the util.CellSample of points_2d (grid-sampled correspondences):
+        every evaluation reads the 4-B cells instead of the pixels
+        (acm_lm_optimize_cells; the same iterates)."""
         L = _lib.load()
         p3 = _as_device_f64(points_3d, 3)
         p2 = _as_device_f64(points_2d, 2)
@@ -120,11 +124,21 @@ class LevenbergMarquardt:
             cb = _lib.ALLREDUCE_FN(allreduce)
         else:
             cb = _lib.ALLREDUCE_FN()
-        _lib.check(L.acm_lm_optimize(ctypes.byref(cam), n, p3.data_ptr() if n else None,
-                                     _lib.LAYOUT_AOS, p2.data_ptr() if n else None,
-                                     ctypes.byref(cfg), cb, ctx,
-                                     ctypes.byref(summ), ws.data_ptr(), ws_bytes,
-                                     _stream_handle()))
+        if cells is not None:
+            if cells.cells.shape[0] != n:
+                raise ValueError("cells and points_3d must have the same number of points")
+            _lib.check(L.acm_lm_optimize_cells(ctypes.byref(cam), n, p3.data_ptr() if n else None,
+                                               _lib.LAYOUT_AOS,
+                                               cells.cells.data_ptr() if n else None,
+                                               ctypes.byref(cells.grid), ctypes.byref(cfg), cb,
+                                               ctx, ctypes.byref(summ), ws.data_ptr(), ws_bytes,
+                                               _stream_handle()))
+        else:
+            _lib.check(L.acm_lm_optimize(ctypes.byref(cam), n, p3.data_ptr() if n else None,
+                                         _lib.LAYOUT_AOS, p2.data_ptr() if n else None,
+                                         ctypes.byref(cfg), cb, ctx,
+                                         ctypes.byref(summ), ws.data_ptr(), ws_bytes,
+                                         _stream_handle()))
         params = list(cam.params)[: model.NUM_PARAMS]
         model._set_params(params)
         return LmResult(parameters=params, iterations=summ.iterations,

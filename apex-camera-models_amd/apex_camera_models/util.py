@@ -36,29 +36,54 @@ class ProjectionError:
     n_valid: int = 0
 
 
-def sample_points(camera_model: CameraModel, n: int, reference_newton: bool = False):
+@dataclass
+class CellSample:
+    """The cell form of grid-sampled correspondences (r06): cells[k] = i * ncx
+    + j is the grid cell of points_2d[k] (point_sampling.rs:56-78), a uint32
+    instead of the 16-B pixel -- what conversion.convert(cells=...) hands the
+    LM (acm_lm_optimize_cells: the same iterates, 12 B per point less read per
+    evaluation)."""
+    cells: torch.Tensor  # (M,) int32 device tensor holding the uint32 cell ids
+    grid: object         # _lib.CellGrid
+
+
+def sample_points(camera_model: CameraModel, n: int, reference_newton: bool = False,
+                  cells: bool = False, cell_range=None):
     """Grid of ~n pixel-cell centres, unprojected; keeps Ok && z > 0, in order.
 
-    Returns (points_2d (M,2), points_3d (M,3)) float64 device tensors.
-    reference_newton=True: ACM_REFERENCE_NEWTON for this call.
+    Returns (points_2d (M,2), points_3d (M,3)) float64 device tensors, and
+    with cells=True a third item, the CellSample of the same points.
+    reference_newton=True: ACM_REFERENCE_NEWTON for this call.  cell_range:
+    (begin, end) cells of the grid (a multi-GPU shard), default all.
     """
     L = _lib.load()
     cam = camera_model.acm_camera()
     ncx, ncy = ctypes.c_uint32(), ctypes.c_uint32()
     _lib.check(L.acm_sample_points_grid(cam.width, cam.height, n, ctypes.byref(ncx),
                                         ctypes.byref(ncy)))
-    cap = ncx.value * ncy.value
+    c0, c1 = cell_range if cell_range is not None else (0, ncx.value * ncy.value)
+    cap = max(c1 - c0, 1)
     dev = torch.device("cuda")
     uv = torch.empty((cap, 2), dtype=torch.float64, device=dev)
     xyz = torch.empty((cap, 3), dtype=torch.float64, device=dev)
     counts = torch.zeros((2,), dtype=torch.int64, device=dev)
     ws_bytes = L.acm_sample_points_workspace_size(ctypes.byref(cam), n)
     ws = torch.empty(((ws_bytes + 7) // 8,), dtype=torch.float64, device=dev)
-    _lib.check(L.acm_sample_points_ex(ctypes.byref(cam), n, 0, cap,
-                                      _lib.REFERENCE_NEWTON if reference_newton else 0,
-                                      uv.data_ptr(), xyz.data_ptr(), counts.data_ptr(),
-                                      ws.data_ptr(), ws_bytes, _stream_handle()))
+    flags = _lib.REFERENCE_NEWTON if reference_newton else 0
+    cl = None
+    if cells:
+        cl = torch.empty((cap,), dtype=torch.int32, device=dev)
+        _lib.check(L.acm_sample_points_cells(ctypes.byref(cam), n, c0, c1, flags, uv.data_ptr(),
+                                             xyz.data_ptr(), cl.data_ptr(), counts.data_ptr(),
+                                             ws.data_ptr(), ws_bytes, _stream_handle()))
+    else:
+        _lib.check(L.acm_sample_points_ex(ctypes.byref(cam), n, c0, c1, flags, uv.data_ptr(),
+                                          xyz.data_ptr(), counts.data_ptr(), ws.data_ptr(),
+                                          ws_bytes, _stream_handle()))
     m = int(counts[0].item())
+    if cells:
+        grid = _lib.CellGrid(ncx.value, ncy.value, cam.width, cam.height)
+        return uv[:m], xyz[:m], CellSample(cl[:m], grid)
     return uv[:m], xyz[:m]
 
 

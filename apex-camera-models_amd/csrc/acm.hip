@@ -1105,15 +1105,55 @@ struct NeAccum {
     }
 };
 
+// Observation streams of k_normal_eq (r06).  ObsPixels: the caller's 2 x N
+// pixels (16 B per point).  ObsCells: grid-sampled correspondences given by
+// their cell index (4 B per point; acm_sample_points_cells): the pixel is
+// the cell centre, recomputed exactly as sample_points wrote it --
+// ((j + 0.5) * cw, (i + 0.5) * ch), point_sampling.rs:66-70 -- so the sums
+// are the pixel form's bit for bit with 12 B per point fewer to read.
+struct ObsPixels {
+    const double* p;
+    using raw = double2;
+    template <bool NTL>
+    __device__ __forceinline__ raw load(size_t i) const { return ld2<NTL>(p + 2 * i); }
+    __device__ __forceinline__ double2 get(raw r) const { return r; }
+    __device__ __forceinline__ static raw zero() { return make_double2(0.0, 0.0); }
+};
+struct ObsCells {
+    const uint32_t* p;
+    uint32_t ncx;
+    double inv_ncx, cw, ch;  // RN(1 / ncx); width / ncx, height / ncy
+    using raw = uint32_t;
+    template <bool NTL>
+    __device__ __forceinline__ raw load(size_t i) const {
+        if (NTL) return __builtin_nontemporal_load(p + i);
+        return p[i];
+    }
+    // c = i ncx + j: the f64 quotient is within 2^-52 (relative) of c / ncx
+    // (c, ncx < 2^32), so its truncation is i, or i - 1 when c / ncx is an
+    // integer approached from below -- one correction
+    __device__ __forceinline__ double2 get(uint32_t c) const {
+        uint32_t i = (uint32_t)((double)c * inv_ncx);
+        uint32_t j = c - i * ncx;
+        if (j >= ncx) {
+            ++i;
+            j -= ncx;
+        }
+        return make_double2(((double)j + 0.5) * cw, ((double)i + 0.5) * ch);
+    }
+    __device__ __forceinline__ static raw zero() { return 0u; }
+};
+
 // WAVES: minimum waves per SIMD the register allocator must allow
 // (amdgpu_waves_per_eu).  1 leaves it free (KB lands at 176 VGPRs = 2 waves);
 // 3 fits KB in 168 without spills; 4 forces 128 with scratch spills for KB and
 // RadTan.  Selected per launch by ACM_TUNE_NE_WAVES (results identical).
-template <class TagT, int LAYOUT, int WAVES, int U, bool NTL>
+template <class TagT, int LAYOUT, int WAVES, int U, bool NTL, class OBS = ObsPixels>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq(acm_camera cam, size_t n,
                                                       const double* __restrict__ pts,
-                                                      const double* __restrict__ obs, int policy,
+                                                      OBS obs, int policy,
                                                       double* __restrict__ parts) {
+    using ORaw = typename OBS::raw;
     using Acc = NeAccum<TagT>;
     constexpr int K = Acc::K;
     const Cam<double> c = make_cam<double>(cam);
@@ -1127,8 +1167,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // ACM_TUNE_NE_UNROLL).  Not for the largest accumulator sets (KB,
     // RadTan), where the extra registers cost a wave of occupancy.
     constexpr bool kPrefetch = K <= 40;
-    auto accumulate = [&](double px, double py, double pz, double2 po) {
-        sums.add(c, px, py, pz, po, sent2);
+    auto accumulate = [&](double px, double py, double pz, ORaw po) {
+        sums.add(c, px, py, pz, obs.get(po), sent2);
     };
     if constexpr (U >= 3) {
         // one point per lane step, loads issued A = U - 1 steps ahead (A
@@ -1140,14 +1180,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         // counted vmcnt of the slot's own load.
         constexpr int A = U - 1;
         double xs[A], ys[A], zs[A];
-        double2 os[A];
+        ORaw os[A];
         // branch-free loads (past the end: point n - 1 again, never
         // accumulated): with loads under exec branches the compiler cannot
         // count them and waits vmcnt(0)
         auto load_slot = [&](int q, size_t iq) {
             const size_t ic = iq < n ? iq : n - 1;
             load_point<LAYOUT, NTL>(pts, n, ic, xs[q], ys[q], zs[q]);
-            os[q] = ld2<NTL>(obs + 2 * ic);
+            os[q] = obs.template load<NTL>(ic);
         };
         if (n) {  // (n = 0: nothing to load, the loop below does not run)
 #pragma unroll
@@ -1163,23 +1203,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         }
     } else if constexpr (U == 1) {
         double x = 0, y = 0, z = 1;
-        double2 o = make_double2(0.0, 0.0);
+        ORaw o = OBS::zero();
         if (kPrefetch && i < n) {
             load_point<LAYOUT, NTL>(pts, n, i, x, y, z);
-            o = ld2<NTL>(obs + 2 * i);
+            o = obs.template load<NTL>(i);
         }
         for (; i < n; i += stride) {
             const size_t inext = i + stride;
             double xn = 0, yn = 0, zn = 1;
-            double2 on = make_double2(0.0, 0.0);
+            ORaw on = OBS::zero();
             if (kPrefetch) {
                 if (inext < n) {
                     load_point<LAYOUT, NTL>(pts, n, inext, xn, yn, zn);
-                    on = ld2<NTL>(obs + 2 * inext);
+                    on = obs.template load<NTL>(inext);
                 }
             } else {
                 load_point<LAYOUT, NTL>(pts, n, i, x, y, z);
-                o = ld2<NTL>(obs + 2 * i);
+                o = obs.template load<NTL>(i);
             }
             accumulate(x, y, z, o);
             if (kPrefetch) { x = xn; y = yn; z = zn; o = on; }
@@ -1188,20 +1228,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         // each wave streams contiguous chunks of U x 64 points (loads in
         // flight a grid stride apart cost DRAM locality, tools/hbm_ceiling.py)
         double x[U], y[U], z[U], xn[U], yn[U], zn[U];
-        double2 o[U], on[U];
+        ORaw o[U], on[U];
         const int lane = threadIdx.x & 63;
         const size_t nw = (size_t)gridDim.x * (kBlock / 64);
         constexpr size_t C = (size_t)U * 64;
         auto load = [&](size_t base, double (&xs)[U], double (&ys)[U], double (&zs)[U],
-                        double2 (&os)[U]) {
+                        ORaw (&os)[U]) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const size_t j = base + (size_t)u * 64 + lane;
                 xs[u] = 0.0; ys[u] = 0.0; zs[u] = 1.0;
-                os[u] = make_double2(0.0, 0.0);
+                os[u] = OBS::zero();
                 if (j < n) {
                     load_point<LAYOUT, NTL>(pts, n, j, xs[u], ys[u], zs[u]);
-                    os[u] = ld2<NTL>(obs + 2 * j);
+                    os[u] = obs.template load<NTL>(j);
                 }
             }
         };
@@ -2097,7 +2137,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
                                                       const uint64_t* __restrict__ blk_off,
                                                       double* __restrict__ uv_out,
                                                       double* __restrict__ xyz_out,
-                                                      const uint64_t* __restrict__ total) {
+                                                      const uint64_t* __restrict__ total,
+                                                      uint32_t* __restrict__ cells_out) {
     static_assert(kSegPerBlock % (4 * SPW) == 0, "write workgroups tile the count blocks");
     if constexpr (FIX) {
         if (total[0] == (uint64_t)cells) return;  // every cell kept: all in place
@@ -2157,6 +2198,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         const uint32_t rank = (uint32_t)__popcll(m & below);
         if (keep) {
             st2<NT>(uv_out + 2 * (off + rank), u, v);  // 16 B per lane, one run per wave
+            if (cells_out) cells_out[off + rank] = cw.i * g.ncx + cw.j;  // (r06) the cell form
             double* d = lx + 3 * rank;
             d[0] = X;
             d[1] = Y;
@@ -2202,7 +2244,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_spec(CamArg cam, Grid g, size_t 
                                                      uint32_t* __restrict__ seg_cnt,
                                                      uint64_t* __restrict__ blk_sum,
                                                      double* __restrict__ uv_out,
-                                                     double* __restrict__ xyz_out) {
+                                                     double* __restrict__ xyz_out,
+                                                     uint32_t* __restrict__ cells_out) {
     // one workgroup per count block (256 segments), wave w takes segments
     // w, w + 4, ... so the four waves write adjacent runs at the same time
     constexpr int SPW = kSegPerBlock / 4;
@@ -2236,6 +2279,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_spec(CamArg cam, Grid g, size_t 
         const uint32_t rank = (uint32_t)__popcll(m & below);
         if (keep) {
             st2<false>(uv_out + 2 * (off + rank), u, v);
+            if (cells_out) cells_out[off + rank] = cw.i * g.ncx + cw.j;
             double* d = lx + 3 * rank;
             d[0] = X;
             d[1] = Y;
@@ -4514,17 +4558,39 @@ ACM_API size_t acm_normal_equations_workspace_size(int model, size_t n) {
 extern "C++" {
 namespace acm {
 // flag / seq: see k_ne_finish_cols / k_ne_publish (the LM's polled path in solver.hip)
+// cells / grid (r06): the observations as grid cells (ObsCells) instead of
+// pixels; the kernel is then the per-model default (NE_WAVES / NE_UNROLL do
+// not apply), which is what makes its sums the pixel form's bit for bit.
+int check_cell_grid(const acm_cell_grid* grid) {
+    if (!grid) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL cell grid");
+    if (!grid->num_cells_x || !grid->num_cells_y || !grid->width || !grid->height ||
+        (uint64_t)grid->num_cells_x * grid->num_cells_y > 0xFFFFFFFFull)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "cell grid: empty, or more than 2^32 - 1 cells");
+    return ACM_SUCCESS;
+}
+static ObsCells obs_cells(const uint32_t* cells, const acm_cell_grid& g) {
+    ObsCells o;
+    o.p = cells;
+    o.ncx = g.num_cells_x;
+    o.inv_ncx = 1.0 / (double)g.num_cells_x;
+    o.cw = (double)g.width / (double)g.num_cells_x;   // point_sampling.rs:57-58, as
+    o.ch = (double)g.height / (double)g.num_cells_y;  // acm_sample_points_ex computes them
+    return o;
+}
 int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                           const double* points_2d_obs, int invalid_policy, double* result,
                           void* workspace, size_t workspace_bytes, void* stream,
                           unsigned long long* flag, unsigned long long seq,
-                          unsigned int* ticket) {
+                          unsigned int* ticket, const uint32_t* cells,
+                          const acm_cell_grid* grid) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
     if (invalid_policy != ACM_INVALID_SKIP && invalid_policy != ACM_INVALID_SENTINEL)
         return fail(ACM_ERR_INVALID_ARGUMENT, "invalid_policy must be SKIP or SENTINEL");
-    if (!result || !workspace || (n && (!points_3d || !points_2d_obs)))
+    if (cells && (rc = check_cell_grid(grid))) return rc;
+    if (!result || !workspace || (n && (!points_3d || !(cells ? (const void*)cells
+                                                               : (const void*)points_2d_obs))))
         return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
     if (workspace_bytes < acm_normal_equations_workspace_size(cam->model, n))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "normal-equations workspace too small");
@@ -4540,6 +4606,21 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
         const int wv0 = g_ne_waves, un0 = g_ne_unroll;
         const int wv = wv0 ? wv0 : Def::W;
         const int un = un0 ? un0 : Def::U;
+        auto go_cells = [&](auto lay_c) {
+            constexpr int LAY = decltype(lay_c)::value;
+            const bool ntl = g_nt_loads != 0;
+            auto kern = ntl ? k_normal_eq<TagT, LAY, Def::W, Def::U, true, ObsCells>
+                            : k_normal_eq<TagT, LAY, Def::W, Def::U, false, ObsCells>;
+            // the pixel form's workgroup count (its occupancy, not the cell
+            // form's): the same grid-stride partition of the points, so the
+            // same summation order and the same bits
+            auto kpix = ntl ? k_normal_eq<TagT, LAY, Def::W, Def::U, true, ObsPixels>
+                            : k_normal_eq<TagT, LAY, Def::W, Def::U, false, ObsPixels>;
+            const int cap = resident_blocks(reinterpret_cast<const void*>(kpix));
+            if (nb > cap) nb = cap;
+            hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
+                               obs_cells(cells, *grid), invalid_policy, parts);
+        };
         auto go = [&](auto lay_c, auto w_c) {
             constexpr int LAY = decltype(lay_c)::value, W = decltype(w_c)::value;
             const bool ntl = g_nt_loads != 0;
@@ -4556,7 +4637,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
-                               points_2d_obs, invalid_policy, parts);
+                               ObsPixels{points_2d_obs}, invalid_policy, parts);
         };
         auto by_waves = [&](auto lay_c) {
             switch (wv) {
@@ -4565,8 +4646,14 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
             default: go(lay_c, std::integral_constant<int, 3>{}); break;
             }
         };
-        if (layout == ACM_LAYOUT_AOS) by_waves(std::integral_constant<int, ACM_LAYOUT_AOS>{});
-        else by_waves(std::integral_constant<int, ACM_LAYOUT_SOA>{});
+        if (cells) {
+            if (layout == ACM_LAYOUT_AOS) go_cells(std::integral_constant<int, ACM_LAYOUT_AOS>{});
+            else go_cells(std::integral_constant<int, ACM_LAYOUT_SOA>{});
+        } else if (layout == ACM_LAYOUT_AOS) {
+            by_waves(std::integral_constant<int, ACM_LAYOUT_AOS>{});
+        } else {
+            by_waves(std::integral_constant<int, ACM_LAYOUT_SOA>{});
+        }
         // (r04) with a ticket the finish kernel's last workgroup releases
         // the completion word itself: one launch fewer per LM evaluation
         // (host loop 1.275 -> 1.252 ms at config 3, three interleaved runs,
@@ -4593,7 +4680,22 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
                                  void* stream) {
     return acm::normal_equations_impl(cam, n, points_3d, layout, points_2d_obs, invalid_policy,
                                       result, workspace, workspace_bytes, stream, nullptr, 0,
-                                      nullptr);
+                                      nullptr, nullptr, nullptr);
+}
+
+ACM_API int acm_normal_equations_cells(const acm_camera* cam, size_t n, const double* points_3d,
+                                       int layout, const uint32_t* cells,
+                                       const acm_cell_grid* grid, int invalid_policy,
+                                       double* result, void* workspace, size_t workspace_bytes,
+                                       void* stream) {
+    if (n && !cells) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (!cells) {  // n = 0: nothing is read
+        static const uint32_t none = 0;
+        cells = &none;
+    }
+    return acm::normal_equations_impl(cam, n, points_3d, layout, nullptr, invalid_policy,
+                                      result, workspace, workspace_bytes, stream, nullptr, 0,
+                                      nullptr, cells, grid);
 }
 
 ACM_API size_t acm_reprojection_stats_workspace_size(size_t n) {
@@ -4748,10 +4850,53 @@ ACM_API size_t acm_sample_points_workspace_size(const acm_camera* cam, size_t n_
     return sample_ws_words((size_t)ncx * ncy) * sizeof(uint64_t);
 }
 
+// The cell form of the kept pixels for the sample_points paths whose write
+// kernels do not emit it (ACM_TUNE_SAMPLE_FUSED 0-3): j = u / cw - 0.5 and
+// i = v / ch - 0.5 rounded -- exact, since u = RN((j + 0.5) cw) is within
+// half an ulp of the centre and the cells are a whole cw apart.
+__global__ __launch_bounds__(kBlock) void k_cells_of_uv(const double* __restrict__ uv,
+                                                        const uint64_t* __restrict__ counts,
+                                                        Grid g, uint32_t* __restrict__ cells_out) {
+    const size_t n = counts[0];
+    for (size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x; t < n;
+         t += (size_t)gridDim.x * kBlock) {
+        const double2 p = ld2<false>(uv + 2 * t);
+        const uint32_t j = (uint32_t)rint(p.x / g.cw - 0.5);
+        const uint32_t i = (uint32_t)rint(p.y / g.ch - 0.5);
+        cells_out[t] = i * g.ncx + j;
+    }
+}
+
+static int sample_points_impl(const acm_camera* cam, size_t n_requested, size_t cell_begin,
+                              size_t cell_end, int flags, double* points_2d_out,
+                              double* points_3d_out, uint32_t* cells_out, uint64_t* counts,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
 ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size_t cell_begin,
                                  size_t cell_end, int flags, double* points_2d_out,
                                  double* points_3d_out, uint64_t* counts, void* workspace,
                                  size_t workspace_bytes, void* stream) {
+    return sample_points_impl(cam, n_requested, cell_begin, cell_end, flags, points_2d_out,
+                              points_3d_out, nullptr, counts, workspace, workspace_bytes, stream);
+}
+
+// (r06) the same, also writing each kept point's cell c = i * ncx + j
+// (cells_out: device uint32[cap]) for the cell forms of the solver
+// (acm_lm_optimize_cells); the grid must have at most 2^32 - 1 cells
+ACM_API int acm_sample_points_cells(const acm_camera* cam, size_t n_requested, size_t cell_begin,
+                                    size_t cell_end, int flags, double* points_2d_out,
+                                    double* points_3d_out, uint32_t* cells_out, uint64_t* counts,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+    if (!cells_out) return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    return sample_points_impl(cam, n_requested, cell_begin, cell_end, flags, points_2d_out,
+                              points_3d_out, cells_out, counts, workspace, workspace_bytes,
+                              stream);
+}
+
+static int sample_points_impl(const acm_camera* cam, size_t n_requested, size_t cell_begin,
+                              size_t cell_end, int flags, double* points_2d_out,
+                              double* points_3d_out, uint32_t* cells_out, uint64_t* counts,
+                              void* workspace, size_t workspace_bytes, void* stream) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if (flags & ~ACM_REFERENCE_NEWTON)
@@ -4770,6 +4915,8 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
     if (workspace_bytes < sample_ws_words(cells) * sizeof(uint64_t))
         return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "sample_points workspace too small");
     if (nt > 0x7fffffffull) return fail(ACM_ERR_INVALID_ARGUMENT, "sample grid too large");
+    if (cells_out && total > 0xFFFFFFFFull)
+        return fail(ACM_ERR_INVALID_ARGUMENT, "cell form: the grid has more than 2^32 - 1 cells");
     Grid g;
     g.ncx = ncx;
     g.ncy = ncy;
@@ -4844,11 +4991,12 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
                 const size_t nwb = (nseg + 4 * (size_t)spw - 1) / (4 * (size_t)spw);
                 hipLaunchKernelGGL(kern, dim3((unsigned)nwb), dim3(kBlock), 0, s, ca, g, cells,
                                    seg_cnt, blk_off, points_2d_out, points_3d_out,
-                                   (const uint64_t*)counts);
+                                   (const uint64_t*)counts, cells_out);
             };
             if (spec) {
                 hipLaunchKernelGGL((k_seg_spec<TagT>), dim3((unsigned)nsb), dim3(kBlock), 0, s, ca,
-                                   g, cells, seg_cnt, blk_sum, points_2d_out, points_3d_out);
+                                   g, cells, seg_cnt, blk_sum, points_2d_out, points_3d_out,
+                                   cells_out);
                 hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, blk_sum, nsb, blk_off,
                                    counts, (uint64_t)cells);
                 wlaunch(k_seg_write<TagT, 16, true, false, true>, 16);
@@ -4879,6 +5027,9 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
             if (rr == 8) kern = k_sample_fused<TagT, 8>;
             hipLaunchKernelGGL(kern, dim3((unsigned)ntr), dim3(kBlock), 0, s, ca, g, cells,
                                status, points_2d_out, points_3d_out, counts);
+            if (cells_out)
+                hipLaunchKernelGGL(k_cells_of_uv, dim3((unsigned)std::min<size_t>(nb, 4096)),
+                                   dim3(kBlock), 0, s, points_2d_out, counts, g, cells_out);
             return check_launch("acm_sample_points");
         });
     }
@@ -4892,6 +5043,9 @@ ACM_API int acm_sample_points_ex(const acm_camera* cam, size_t n_requested, size
                            (uint64_t)cells);
         hipLaunchKernelGGL((k_sample_write<TagT>), dim3((unsigned)nb), dim3(kBlock), 0, s, ca, g,
                            cells, off, points_2d_out, points_3d_out);
+        if (cells_out)
+            hipLaunchKernelGGL(k_cells_of_uv, dim3((unsigned)std::min<size_t>(nb, 4096)),
+                               dim3(kBlock), 0, s, points_2d_out, counts, g, cells_out);
         return check_launch("acm_sample_points");
     });
 }

@@ -314,6 +314,33 @@ __device__ __forceinline__ T div_shared(const T (&a)[K], T b, T (&q)[K]) {
     return y;
 }
 
+// a / b given y = RN(1 / b) from an earlier div_shared by the same b: the
+// same correctly rounded quotient, or the IEEE division outside the range
+template <class T>
+__device__ __forceinline__ T div_by_y(T a, T b, T y) {
+    if constexpr (sizeof(T) == 8) {
+        if (div_safe(a) && div_safe(b)) return div_rn(a, y, b);
+    }
+    return a / b;
+}
+
+// (r06) the projections' two divisions by one divisor
+// (x / z, y / z; x / denom, y / denom) as one IEEE reciprocal and two
+// Markstein corrections: RN(x / b), RN(y / b) bit for bit (div_shared).
+// One v_rcp_f64 and division sequence fewer per point, but the operands'
+// range tests cost about what that saves: RadTan's round trip measured
+// even (0.628 vs 0.632 ms at 50M, profiles/r06e_ab.log); the +J forms
+// share the reciprocal with their two further divisions (div_by_y).
+template <class T>
+__device__ __forceinline__ T div2(T x, T y, T b, T& qx, T& qy) {
+    const T a[2] = {x, y};
+    T q[2];
+    const T r = div_shared(a, b, q);
+    qx = q[0];
+    qy = q[1];
+    return r;
+}
+
 template <class T>
 __device__ __forceinline__ bool norm_below_1e6(T sq) {
     if constexpr (sizeof(T) == 8) return sq < T(kNewtonTol2);
@@ -379,14 +406,29 @@ struct Pinhole {
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
         const T iz = FAST ? T(1) / z : T(0);
-        u = FAST ? fx * (x * iz) + cx : fx * x / z + cx;  // :170
-        v = FAST ? fy * (y * iz) + cy : fy * y / z + cy;  // :171
+        T fxx, fyy, rz = T(0);  // fx * x / z is (fx * x) / z (:170-171)
+        if (FAST) {
+            fxx = fx * (x * iz);
+            fyy = fy * (y * iz);
+        } else {
+            rz = div2(fx * x, fy * y, z, fxx, fyy);
+        }
+        u = fxx + cx;  // :170
+        v = fyy + cy;  // :171
         uint8_t st = ST_OK;
         if (u < T(0) || u >= c.w || v < T(0) || v >= c.h) st = ST_PROJECTION_OUT_SIDE_IMAGE;
         if (z < T(kEpsSqrt)) st = ST_POINT_AT_CAMERA_CENTER;  // :167, checked first
         if (WJ) {
-            ju[0] = FAST ? x * iz : x / z; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
-            jv[0] = T(0); jv[1] = FAST ? y * iz : y / z; jv[2] = T(0); jv[3] = T(1);
+            T xz, yz;
+            if (FAST) {
+                xz = x * iz;
+                yz = y * iz;
+            } else {  // x / z, y / z from the same reciprocal
+                xz = div_by_y(x, z, rz);
+                yz = div_by_y(y, z, rz);
+            }
+            ju[0] = xz; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
+            jv[0] = T(0); jv[1] = yz; jv[2] = T(0); jv[3] = T(1);
         }
         return st;
     }
@@ -418,7 +460,13 @@ struct RadTan {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
         const T k1 = c.p[4], k2 = c.p[5], p1 = c.p[6], p2 = c.p[7], k3 = c.p[8];
         const T iz = FAST ? T(1) / z : T(0);
-        T xp = FAST ? x * iz : x / z, yp = FAST ? y * iz : y / z;
+        T xp, yp;
+        if (FAST) {
+            xp = x * iz;
+            yp = y * iz;
+        } else {
+            div2(x, y, z, xp, yp);  // x / z, y / z (:315-316)
+        }
         T r2 = xp * xp + yp * yp;
         T r4 = r2 * r2;
         T r6 = r4 * r2;
@@ -681,6 +729,7 @@ struct RadTan {
         }
         return newton_finish(s, X, Y, Z);
     }
+
 };
 
 // --------------------------------------------------------- Kannala-Brandt
@@ -1061,6 +1110,22 @@ struct KannalaBrandt {
             // decision depends on it, and the ray is held to 1e-10 anyway
             // (sin / cos are polynomials).  1 / ru and 1 / |p| from rcp / rsq
             // + Newton (~1 ulp) instead of two IEEE divisions and a sqrt.
+#ifndef ACM_AB_KB_NORMALIZE  // A/B build: normalise every certified ray (r05)
+            if (certified && ru < T(kPi / 2.0)) {
+                // (r06) not clamped: ru = |m| (to ~1 ulp, from rsq) and
+                // (sin(theta) m / ru, cos(theta)) is a unit vector up to
+                // rounding, so the reference's normalize() (:545-561) moves
+                // it by ~1 ulp: no |p|, no rsq -- the 16 VALU instructions of
+                // the normalisation, ~5% of the KB round trip.  (The clamped
+                // ray, ru = pi/2 < |m|, is not unit: normalised below.)
+                const T q = s * ir_fast;  // sin(theta) / ru
+                X = mx * q;
+                Y = my * q;
+                Z = co;
+                keep = converged && cos_pos;
+                return ST_OK;
+            }
+#endif
             const T ir = certified ? ir_fast : (nr_range(ru) ? rcp_nr(ru) : T(1) / ru);
             const T xc = small ? T(0) : mx * ir;  // mx / ru
             const T yc = small ? T(0) : my * ir;
@@ -1115,11 +1180,18 @@ struct DoubleSphere {
         const T w2 = c.uk[1];
         const bool ok = !(denom < T(1e-3)) && (z > -w2 * d1);
         const T id = FAST ? T(1) / denom : T(0);
-        T mx = FAST ? x * id : x / denom, my = FAST ? y * id : y / denom;
+        T mx, my, yd = T(0);
+        if (FAST) {
+            mx = x * id;
+            my = y * id;
+        } else {
+            yd = div2(x, y, denom, mx, my);  // x / denom, y / denom (:383-384)
+        }
         u = fx * (mx) + cx;
         v = fy * (my) + cy;
         if (WJ) {
-            T tu = FAST ? fx * mx * id : fx * mx / denom, tv = FAST ? fy * my * id : fy * my / denom;
+            T tu = FAST ? fx * mx * id : div_by_y(fx * mx, denom, yd);
+            T tv = FAST ? fy * my * id : div_by_y(fy * my, denom, yd);
             T dda = d2 - gamma;
             T ddx = d1 * (alpha * gamma / d2 + (T(1) - alpha));
             ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);
@@ -1173,11 +1245,18 @@ struct Ucm {
         const T w = c.uk[2];  // per camera (acm.hip unproject_consts, r05)
         const bool ok = !(denom < T(1e-3)) && (z > -w * d);
         const T id = FAST ? T(1) / denom : T(0);
-        T mx = FAST ? x * id : x / denom, my = FAST ? y * id : y / denom;
+        T mx, my, yd = T(0);
+        if (FAST) {
+            mx = x * id;
+            my = y * id;
+        } else {
+            yd = div2(x, y, denom, mx, my);  // x / denom, y / denom
+        }
         u = fx * mx + cx;
         v = fy * my + cy;
         if (WJ) {
-            T tu = FAST ? fx * mx * id : fx * mx / denom, tv = FAST ? fy * my * id : fy * my / denom;
+            T tu = FAST ? fx * mx * id : div_by_y(fx * mx, denom, yd);
+            T tv = FAST ? fy * my * id : div_by_y(fy * my, denom, yd);
             T dda = d - z;
             ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0); ju[4] = -tu * dda;
             jv[0] = T(0); jv[1] = my; jv[2] = T(0); jv[3] = T(1); jv[4] = -tv * dda;
@@ -1230,11 +1309,18 @@ struct Eucm {
         }
         const bool ok = !(denom < T(1e-3)) && cond;
         const T id = FAST ? T(1) / denom : T(0);
-        T mx = FAST ? x * id : x / denom, my = FAST ? y * id : y / denom;
+        T mx, my, yd = T(0);
+        if (FAST) {
+            mx = x * id;
+            my = y * id;
+        } else {
+            yd = div2(x, y, denom, mx, my);  // x / denom, y / denom
+        }
         u = fx * mx + cx;
         v = fy * my + cy;
         if (WJ) {
-            T tu = FAST ? fx * mx * id : fx * mx / denom, tv = FAST ? fy * my * id : fy * my / denom;
+            T tu = FAST ? fx * mx * id : div_by_y(fx * mx, denom, yd);
+            T tv = FAST ? fy * my * id : div_by_y(fy * my, denom, yd);
             T dda = d - z;
             T ddb = alpha * rr / (T(2) * d);
             ju[0] = mx; ju[1] = T(0); ju[2] = T(1); ju[3] = T(0);

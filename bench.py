@@ -573,7 +573,10 @@ def leg_config5(ctx, n_cells):
     kp, (w, h) = samples.SAMPLES[2]
     src = KannalaBrandtModel._from_params(kp, Resolution(w, h))
     from apex_camera_models import _lib
-    fn = D.gpu_sample_points_range(src, n_cells)
+    # (r06) the cell form: sample_points also writes each kept point's grid
+    # cell, and the LM's evaluations read those 4 B instead of the 16-B pixel
+    # (acm_lm_optimize_cells; the same iterates, bit for bit)
+    fn = D.gpu_sample_points_range(src, n_cells, cells=True)
     gx, gy = ctypes.c_uint32(), ctypes.c_uint32()  # the grid acm_sample_points uses
     _lib.check(_lib.load().acm_sample_points_grid(w, h, n_cells, ctypes.byref(gx),
                                                   ctypes.byref(gy)))
@@ -581,17 +584,17 @@ def leg_config5(ctx, n_cells):
 
     def sample():
         if ctx.dist:
-            uv, xyz, _, total = D.sharded_sample_points(ncx, ncy, ctx.rank, ctx.world, fn)
+            uv, xyz, cl, _, total = D.sharded_sample_points(ncx, ncy, ctx.rank, ctx.world, fn)
         else:
-            uv, xyz = fn(0, ncx * ncy)
+            uv, xyz, cl = fn(0, ncx * ncy)
             total = int(uv.shape[0])
-        return uv, xyz, total
+        return uv, xyz, cl, total
 
-    uv, xyz, _ = sample()  # warm-up: the caching allocator's first multi-GB blocks
-    del uv, xyz
+    uv, xyz, cl, _ = sample()  # warm-up: the caching allocator's first multi-GB blocks
+    del uv, xyz, cl
     ctx.sync()
     t0 = time.perf_counter()
-    uv, xyz, total = sample()
+    uv, xyz, cl, total = sample()
     ctx.sync()
     t_s = ctx.max_over_ranks(time.perf_counter() - t0)
     # N > 1: the sharded conversion over RCCL driven from libacm (r06; gloo
@@ -609,12 +612,12 @@ def leg_config5(ctx, n_cells):
     def timed(c):
         # one untimed conversion first (its multi-GB workspaces' first
         # allocation), then the fastest of three, each the max over ranks
-        conversion.convert(src, "double_sphere", xyz, uv, collective=c)
+        conversion.convert(src, "double_sphere", xyz, uv, collective=c, cells=cl)
         t, m = float("inf"), None
         for _ in range(3):
             ctx.sync()
             t0 = time.perf_counter()
-            m = conversion.convert(src, "double_sphere", xyz, uv, collective=c)
+            m = conversion.convert(src, "double_sphere", xyz, uv, collective=c, cells=cl)
             ctx.sync()
             t = min(t, ctx.max_over_ranks(time.perf_counter() - t0))
         return t, m
@@ -652,7 +655,8 @@ def leg_config5(ctx, n_cells):
             coll.close()
     if world1 is not None:
         out["sharded_world1"] = world1
-    del uv, xyz
+    out["lm_observations"] = "cells (4 B per point, acm_lm_optimize_cells)"
+    del uv, xyz, cl
     torch.cuda.empty_cache()
     return out
 

@@ -126,11 +126,30 @@ def test_config5_kb_to_ds_on_92_9m_correspondences():
     from apex_camera_models import conversion, factors, util
     from apex_camera_models.camera import Resolution
     m, kp, w, h = _kb()
-    uv, xyz = util.sample_points(m, 100_000_000)
+    uv, xyz, cs = util.sample_points(m, 100_000_000, cells=True)
     n = xyz.shape[0]
     assert n == 92_935_075
-    met = conversion.convert(m, "double_sphere", xyz, uv)
+    met = conversion.convert(m, "double_sphere", xyz, uv, cells=cs)
     assert met.convergence_status == "Converged", met.lm_termination
+    # (r06) the cell form at scale: the fused normal equations from the 4-B
+    # cells equal the pixel form's over all 92.9M points, bit for bit
+    import ctypes
+    from apex_camera_models import _lib
+    from apex_camera_models.camera import _stream_handle
+    L = _lib.load()
+    cam = met.model.acm_camera()
+    wsb = L.acm_normal_equations_workspace_size(DS, n)
+    ws = torch.empty(wsb // 8 + 1, dtype=torch.float64, device="cuda")
+    a = torch.empty(44, dtype=torch.float64, device="cuda")
+    b = torch.empty(44, dtype=torch.float64, device="cuda")
+    _lib.check(L.acm_normal_equations(ctypes.byref(cam), n, xyz.data_ptr(), 0, uv.data_ptr(), 0,
+                                      a.data_ptr(), ws.data_ptr(), wsb, _stream_handle()))
+    _lib.check(L.acm_normal_equations_cells(ctypes.byref(cam), n, xyz.data_ptr(), 0,
+                                            cs.cells.data_ptr(), ctypes.byref(cs.grid), 0,
+                                            b.data_ptr(), ws.data_ptr(), wsb, _stream_handle()))
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int64), b.view(torch.int64))
+    del ws, cs
     assert met.final_reprojection_error.n_valid == n
     assert met.final_reprojection_error.mean < 0.02  # README.md:163 reports 0.008 px
     p = met.model.params()

@@ -2,6 +2,7 @@
 config-5 KB -> DS convert() at 1e8 sampled cells, warm, best of --reps,
 
   none   -- conversion.convert(collective=None): the 1-rank path;
+  cells  -- the same with the LM on the cell form (r06, util.CellSample);
   py     -- a 1-rank process group and the torch.distributed callbacks
             (distributed.TorchCollective; before r06: rccl_allreduce);
   rccl   -- a 1-rank RCCL communicator driven from libacm
@@ -40,12 +41,14 @@ def main():
                             device_id=torch.device("cuda", 0))
     kp, (w, h) = samples.SAMPLES[2]
     src = KannalaBrandtModel._from_params(kp, Resolution(w, h))
-    uv, xyz = util.sample_points(src, a.cells)
+    uv, xyz, cs = util.sample_points(src, a.cells, cells=True)
     torch.cuda.synchronize()
     colls = {}
     for m in a.modes.split(","):
-        if m == "none":
+        if m in ("none", "cells"):
             colls[m] = None
+        elif m == "rccl_cells" and hasattr(D, "RcclCollective"):
+            colls[m] = D.RcclCollective()
         elif m == "py" and hasattr(D, "TorchCollective"):
             colls[m] = D.TorchCollective()
         elif m == "py":
@@ -53,21 +56,22 @@ def main():
         elif m == "rccl" and hasattr(D, "RcclCollective"):
             colls[m] = D.RcclCollective()
 
-    def run(c):
+    def run(m, c):
         if c == "legacy":
             return conversion.convert(src, "double_sphere", xyz, uv, allreduce=D.rccl_allreduce())
+        kw = {"cells": cs} if m.endswith("cells") else {}
         if c is None:
-            return conversion.convert(src, "double_sphere", xyz, uv)
-        return conversion.convert(src, "double_sphere", xyz, uv, collective=c)
+            return conversion.convert(src, "double_sphere", xyz, uv, **kw)
+        return conversion.convert(src, "double_sphere", xyz, uv, collective=c, **kw)
 
     best, info = {}, {}
     for m, c in colls.items():  # cold run: workspaces, communicator warm-up
-        run(c)
+        run(m, c)
     for _ in range(a.reps):
         for m, c in colls.items():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            met = run(c)
+            met = run(m, c)
             torch.cuda.synchronize()
             t = (time.perf_counter() - t0) * 1e3
             best[m] = min(best.get(m, float("inf")), t)
