@@ -155,6 +155,8 @@ EXPORTED_SYMBOLS = (
     "acm_lm_workspace_size",
     "acm_lm_optimize",
     "acm_normal_equations_cells",
+    "acm_reprojection_error_cells",
+    "acm_linear_estimation_with_error_cells_async",
     "acm_lm_optimize_cells",
     "acm_sample_points_cells",
     "acm_rccl_available",
@@ -314,6 +316,11 @@ def load():
     L.acm_lm_optimize_cells.restype = i
     L.acm_sample_points_cells.argtypes = [cam_p, sz, sz, sz, i, vp, vp, vp, vp, vp, sz, vp]
     L.acm_sample_points_cells.restype = i
+    L.acm_reprojection_error_cells.argtypes = [cam_p, sz, vp, i, vp, grid_p, vp, vp, vp, sz, vp]
+    L.acm_reprojection_error_cells.restype = i
+    L.acm_linear_estimation_with_error_cells_async.argtypes = [cam_p, sz, vp, i, vp, vp, grid_p,
+                                                              vp, vp, vp, sz, vp]
+    L.acm_linear_estimation_with_error_cells_async.restype = i
     coll_p = ctypes.POINTER(AcmCollective)
     L.acm_rccl_available.argtypes = []
     L.acm_rccl_available.restype = i
@@ -325,12 +332,13 @@ def load():
     L.acm_rccl_destroy.restype = i
     L.acm_linear_estimation_with_error_sharded_workspace_size.argtypes = [i, sz, ctypes.c_int32]
     L.acm_linear_estimation_with_error_sharded_workspace_size.restype = sz
-    L.acm_linear_estimation_with_error_sharded.argtypes = [cam_p, sz, vp, i, vp, vp, vp, coll_p,
-                                                           vp, sz, vp]
+    L.acm_linear_estimation_with_error_sharded.argtypes = [cam_p, sz, vp, i, vp, vp, grid_p, vp,
+                                                           vp, coll_p, vp, sz, vp]
     L.acm_linear_estimation_with_error_sharded.restype = i
     L.acm_reprojection_error_sharded_workspace_size.argtypes = [sz, ctypes.c_int32]
     L.acm_reprojection_error_sharded_workspace_size.restype = sz
-    L.acm_reprojection_error_sharded.argtypes = [cam_p, sz, vp, i, vp, vp, vp, coll_p, vp, sz, vp]
+    L.acm_reprojection_error_sharded.argtypes = [cam_p, sz, vp, i, vp, vp, grid_p, vp, vp, coll_p,
+                                                 vp, sz, vp]
     L.acm_reprojection_error_sharded.restype = i
     L.acm_median_workspace_size.argtypes = [sz]
     L.acm_median_workspace_size.restype = sz

@@ -67,8 +67,9 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
     identically on every rank, with the same structure as on one GPU.
 
     cells (r06): the util.CellSample of points_2d when the correspondences
-    come from sample_points(..., cells=True): the LM's evaluations read the
-    4-B cells instead of the 16-B pixels, with the same iterates."""
+    come from sample_points(..., cells=True): the opening, the LM's
+    evaluations and the final error read the 4-B cells instead of the 16-B
+    pixels -- the same results, bit for bit."""
     import torch
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -76,7 +77,7 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
     # the initial error and the linear estimation in one pass (r04); its
     # median completes on the stream while the LM starts (r05)
     initial, finish_initial = util.initial_error_and_linear_estimation(
-        model, points_3d, points_2d, defer_median=True, collective=collective)
+        model, points_3d, points_2d, defer_median=True, collective=collective, cells=cells)
     cfg = config or LevenbergMarquardtConfig()
     status = "Converged"
     res = None
@@ -97,7 +98,8 @@ def convert(input_model: CameraModel, target: str, points_3d, points_2d,
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
     initial = finish_initial()
-    final = util.compute_reprojection_error(model, points_3d, points_2d, collective=collective)
+    final = util.compute_reprojection_error(model, points_3d, points_2d, collective=collective,
+                                            cells=cells)
     # camera_converter.rs:425-438; failed regions come back as NaN (no raise)
     validation = util.validate_conversion_accuracy(model, input_model)
     return ConversionMetrics(model=model, model_name=DISPLAY[target],

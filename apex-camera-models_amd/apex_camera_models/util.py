@@ -107,14 +107,15 @@ def reprojection_stats(camera_model: CameraModel, points3d, points2d, errors=Non
 
 
 def compute_reprojection_error(camera_model: CameraModel, points3d, points2d,
-                               collective=None) -> ProjectionError:
+                               collective=None, cells=None) -> ProjectionError:
     """error_metrics.rs:62-121: one acm_reprojection_error call (the
     statistics and the median, whose first radix histogram the statistics
     pass counts) and one device -> host read of its 9 doubles.
 
     collective (distributed.RcclCollective / TorchCollective, r06): the
     points are this rank's shard, and the result is the union's
-    (acm_reprojection_error_sharded), the same on every rank."""
+    (acm_reprojection_error_sharded), the same on every rank.  cells (r06):
+    the CellSample of points2d -- the pass reads the 4-B cells (same bits)."""
     L = _lib.load()
     p3 = _as_device_f64(points3d, 3)
     p2 = _as_device_f64(points2d, 2)
@@ -123,13 +124,20 @@ def compute_reprojection_error(camera_model: CameraModel, points3d, points2d,
         raise ValueError("points3d and points2d must have the same number of columns")
     res = torch.empty((9,), dtype=torch.float64, device=p3.device)
     cam = camera_model.acm_camera()
+    cl, grid = _cell_args(cells, n)
     if collective is not None:
         ws_bytes = L.acm_reprojection_error_sharded_workspace_size(n, collective.c.world)
         ws = _workspace(ws_bytes, p3.device)
         _lib.check(L.acm_reprojection_error_sharded(
             ctypes.byref(cam), n, p3.data_ptr() if n else None, _lib.LAYOUT_AOS,
-            p2.data_ptr() if n else None, res.data_ptr(), None, ctypes.byref(collective.c),
-            ws.data_ptr(), ws_bytes, _stream_handle()))
+            p2.data_ptr() if n else None, cl, grid, res.data_ptr(), None,
+            ctypes.byref(collective.c), ws.data_ptr(), ws_bytes, _stream_handle()))
+    elif cells is not None:
+        ws_bytes = L.acm_reprojection_error_workspace_size(n)
+        ws = _workspace(ws_bytes, p3.device)
+        _lib.check(L.acm_reprojection_error_cells(ctypes.byref(cam), n, p3.data_ptr(),
+                                                  _lib.LAYOUT_AOS, cl, grid, res.data_ptr(), None,
+                                                  ws.data_ptr(), ws_bytes, _stream_handle()))
     else:
         ws_bytes = L.acm_reprojection_error_workspace_size(n)
         ws = _workspace(ws_bytes, p3.device)
@@ -148,8 +156,19 @@ def _workspace(nbytes: int, device) -> torch.Tensor:
     return torch.empty(((nbytes + 7) // 8,), dtype=torch.float64, device=device)
 
 
+def _cell_args(cells, n):
+    """(cells pointer, grid reference) for the C-ABI's nullable cell-form
+    arguments (None, None without a CellSample)."""
+    if cells is None:
+        return None, None
+    if cells.cells.shape[0] != n:
+        raise ValueError("cells and points_3d must have the same number of points")
+    return (cells.cells.data_ptr() if n else None), ctypes.byref(cells.grid)
+
+
 def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d,
-                                        defer_median: bool = False, collective=None):
+                                        defer_median: bool = False, collective=None,
+                                        cells=None):
     """convert_to_*'s opening (camera_converter.rs:371-375): the reprojection
     error of `model` as given, then `model.linear_estimation` -- for the TSQR
     models one pass over the correspondences (acm_linear_estimation_with_error_async).
@@ -165,7 +184,8 @@ def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d,
     collective (r06): the points are this rank's shard and everything is
     over the union (acm_linear_estimation_with_error_sharded: one all-gather
     of each rank's factor and statistics, the distributed median); every
-    rank gets the same model."""
+    rank gets the same model.  cells (r06): the CellSample of points2d --
+    the fused pass reads the 4-B cells (same bits)."""
     L = _lib.load()
     p3 = _as_device_f64(points3d, 3)
     p2 = _as_device_f64(points2d, 2)
@@ -184,11 +204,16 @@ def initial_error_and_linear_estimation(model: CameraModel, points3d, points2d,
     res = torch.full((9,), float("nan"), dtype=torch.float64, device=p3.device)
     host = (ctypes.c_double * 8)(*([float("nan")] * 8))
     cam = model.acm_camera()
+    cl, grid = _cell_args(cells, n)
     if collective is not None:
         rc = L.acm_linear_estimation_with_error_sharded(
             ctypes.byref(cam), n, p3.data_ptr() if n else None, _lib.LAYOUT_AOS,
-            p2.data_ptr() if n else None, res.data_ptr(), host, ctypes.byref(collective.c),
-            ws.data_ptr(), ws_bytes, _stream_handle())
+            p2.data_ptr() if n else None, cl, grid, res.data_ptr(), host,
+            ctypes.byref(collective.c), ws.data_ptr(), ws_bytes, _stream_handle())
+    elif cells is not None:
+        rc = L.acm_linear_estimation_with_error_cells_async(
+            ctypes.byref(cam), n, p3.data_ptr(), _lib.LAYOUT_AOS, p2.data_ptr(), cl, grid,
+            res.data_ptr(), host, ws.data_ptr(), ws_bytes, _stream_handle())
     else:
         rc = L.acm_linear_estimation_with_error_async(ctypes.byref(cam), n, p3.data_ptr(),
                                                       _lib.LAYOUT_AOS, p2.data_ptr(),

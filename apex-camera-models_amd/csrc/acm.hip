@@ -1513,10 +1513,10 @@ __device__ __forceinline__ unsigned sel_digit0(double e) {
     return (unsigned)(((unsigned long long)__double_as_longlong(e) >> 53) & (kSelBins - 1));
 }
 
-template <class TagT, int LAYOUT, bool NTL, bool NTS, bool HIST>
+template <class TagT, int LAYOUT, bool NTL, bool NTS, bool HIST, class OBS = ObsPixels>
 __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t n,
                                                          const double* __restrict__ pts,
-                                                         const double* __restrict__ obs,
+                                                         OBS obs,
                                                          double* __restrict__ errs,
                                                          double* __restrict__ parts,
                                                          unsigned int* __restrict__ hparts) {
@@ -1533,11 +1533,11 @@ __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t 
     size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
     constexpr int A = kReprojA;
     double xs[A], ys[A], zs[A];
-    double2 os[A];
+    typename OBS::raw os[A];
     auto load_slot = [&](int q, size_t iq) {
         const size_t ic = iq < n ? iq : n - 1;
         load_point<LAYOUT, NTL>(pts, n, ic, xs[q], ys[q], zs[q]);
-        os[q] = ld2<NTL>(obs + 2 * ic);
+        os[q] = obs.template load<NTL>(ic);
     };
     if (n) {
 #pragma unroll
@@ -1550,7 +1550,7 @@ __global__ __launch_bounds__(kBlock) void k_reproj_pass1(acm_camera cam, size_t 
             const bool in = iq < n;
             double e = __builtin_nan("");
             if (in) {
-                e = reproj_error<M>(c, xs[q], ys[q], zs[q], os[q]);
+                e = reproj_error<M>(c, xs[q], ys[q], zs[q], obs.get(os[q]));
                 acc.add(e);
                 if (NTS) __builtin_nontemporal_store(e, errs + iq);
                 else errs[iq] = e;
@@ -2946,10 +2946,10 @@ template <int M> constexpr int kTsqrB = M <= 3 ? 4 : 2;
 // correspondences (camera_converter.rs:371-375) -- so the 40 B per point are
 // read once for both: per-point errors (errs), k_reproj_pass1's statistics
 // partials (rparts) and the median's pass-0 histogram (hparts).
-template <int MODEL, int LAYOUT, class TagR = void, bool NTS = false, bool NTL = false>
+template <int MODEL, int LAYOUT, class TagR = void, bool NTS = false, bool NTL = false, class OBS = ObsPixels>
 __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
                                                  const double* __restrict__ pts,
-                                                 const double* __restrict__ obs,
+                                                 OBS obs,
                                                  double* __restrict__ parts,
                                                  int* __restrict__ err_flag,
                                                  double* __restrict__ errs,
@@ -2983,11 +2983,11 @@ __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
     constexpr int B = kTsqrB<M>;
     constexpr int A = B * kTsqrRounds;  // load slots: kTsqrRounds batches in flight
     double xs[A], ys[A], zs[A];
-    double2 os[A];
+    typename OBS::raw os[A];
     auto load_slot = [&](int q, size_t iq) {
         const size_t ic = iq < n ? iq : n - 1;
         load_point<LAYOUT, NTL>(pts, n, ic, xs[q], ys[q], zs[q]);
-        os[q] = ld2<NTL>(obs + 2 * ic);
+        os[q] = obs.template load<NTL>(ic);
     };
     size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
     if (n) {
@@ -3003,11 +3003,12 @@ __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
             const int b = g * B + bb;  // slot
             const size_t ib = i + (size_t)b * stride;
             const bool in = ib < n;
+            const double2 ob = obs.get(os[b]);
             if constexpr (REPROJ) {
                 using MR = typename TagR::template type<double>;
                 double e = __builtin_nan("");
                 if (in) {
-                    e = reproj_error<MR>(c, xs[b], ys[b], zs[b], os[b]);
+                    e = reproj_error<MR>(c, xs[b], ys[b], zs[b], ob);
                     acc.add(e);
                     if (NTS) __builtin_nontemporal_store(e, errs + ib);
                     else errs[ib] = e;
@@ -3015,7 +3016,7 @@ __global__ __launch_bounds__(kBlock) void k_tsqr(acm_camera cam, size_t n,
                 sel_count<true>(h, in, sel_digit0(e));
             }
             int e = 0;
-            const bool ok = in && RW::rows(c, xs[b], ys[b], zs[b], os[b].x, os[b].y, rows[2 * bb],
+            const bool ok = in && RW::rows(c, xs[b], ys[b], zs[b], ob.x, ob.y, rows[2 * bb],
                                            rows[2 * bb + 1], e);
             if (in) err |= e;
             if (!ok) {
@@ -4713,7 +4714,8 @@ static int reprojection_stats_impl(const acm_camera* cam, size_t n, const double
                                    int layout, const double* points_2d, double* result,
                                    double* errors, void* workspace, hipStream_t s,
                                    unsigned int* hparts, int* nb_out,
-                                   void* median_ws = nullptr) {
+                                   void* median_ws = nullptr, const uint32_t* cells = nullptr,
+                                   const acm_cell_grid* grid = nullptr) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -4740,8 +4742,23 @@ static int reprojection_stats_impl(const acm_camera* cam, size_t n, const double
                                     : k_reproj_pass1<TagT, LAY, false, true, true>;
             }
             nb1 = std::min(nb1, resident_blocks(reinterpret_cast<const void*>(kern)));
-            hipLaunchKernelGGL(kern, dim3(nb1), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
-                               points_2d, errs, p1, hparts);
+            if (cells) {  // (r06) the cell form, on the pixel form's partition
+                auto kc = ntl ? k_reproj_pass1<TagT, LAY, true, false, false, ObsCells>
+                              : k_reproj_pass1<TagT, LAY, false, false, false, ObsCells>;
+                if (nts) kc = ntl ? k_reproj_pass1<TagT, LAY, true, true, false, ObsCells>
+                                  : k_reproj_pass1<TagT, LAY, false, true, false, ObsCells>;
+                if (hparts) {
+                    kc = ntl ? k_reproj_pass1<TagT, LAY, true, false, true, ObsCells>
+                             : k_reproj_pass1<TagT, LAY, false, false, true, ObsCells>;
+                    if (nts) kc = ntl ? k_reproj_pass1<TagT, LAY, true, true, true, ObsCells>
+                                      : k_reproj_pass1<TagT, LAY, false, true, true, ObsCells>;
+                }
+                hipLaunchKernelGGL(kc, dim3(nb1), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
+                                   acm::obs_cells(cells, *grid), errs, p1, hparts);
+            } else {
+                hipLaunchKernelGGL(kern, dim3(nb1), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
+                                   ObsPixels{points_2d}, errs, p1, hparts);
+            }
         };
         if (layout == ACM_LAYOUT_AOS) go(std::integral_constant<int, ACM_LAYOUT_AOS>{});
         else go(std::integral_constant<int, ACM_LAYOUT_SOA>{});
@@ -5174,7 +5191,7 @@ ACM_API int acm_linear_system_qr(const acm_camera* cam, size_t n, const double* 
         const int nb = std::min((int)tsqr_blocks(n),
                                 resident_blocks(reinterpret_cast<const void*>(kern)));
         hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
-                           points_2d, parts, error_flag, nullptr, nullptr, nullptr);
+                           ObsPixels{points_2d}, parts, error_flag, nullptr, nullptr, nullptr);
         hipLaunchKernelGGL((k_tsqr_final<M>), dim3(1), dim3(kBlock), 0, s, parts, nb, r_factor);
     };
     switch (cam->model) {
@@ -5209,10 +5226,13 @@ namespace acm {
 // hist_nb != nullptr (the sharded opening, sharded.hip): the shard's R, flag
 // and 8 statistics only -- no median state, no host copy, no median; the
 // pass-0 histogram partials stay in ws_err and *hist_nb = their workgroups.
+// cells / grid (r06): the observations in the cell form (ObsCells), the
+// partition of the pixel form's launch (its occupancy), so the same bits.
 int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                            const double* points_2d, double* r_factor, int* error_flag,
                            double* result, void* ws_qr, void* ws_err, void* stream,
-                           double* host_out, hipEvent_t ready, int* hist_nb) {
+                           double* host_out, hipEvent_t ready, int* hist_nb,
+                           const uint32_t* cells, const acm_cell_grid* grid) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -5234,8 +5254,16 @@ int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points
         auto kern = layout == ACM_LAYOUT_AOS ? k_tsqr<MOD, ACM_LAYOUT_AOS, TagR, true, kTsqrNtl>
                                              : k_tsqr<MOD, ACM_LAYOUT_SOA, TagR, true, kTsqrNtl>;
         nb = std::min((int)tsqr_blocks(n), resident_blocks(reinterpret_cast<const void*>(kern)));
-        hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
-                           points_2d, parts, error_flag, errs, p1, hparts);
+        if (cells) {
+            auto kc = layout == ACM_LAYOUT_AOS
+                          ? k_tsqr<MOD, ACM_LAYOUT_AOS, TagR, true, kTsqrNtl, ObsCells>
+                          : k_tsqr<MOD, ACM_LAYOUT_SOA, TagR, true, kTsqrNtl, ObsCells>;
+            hipLaunchKernelGGL(kc, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
+                               obs_cells(cells, *grid), parts, error_flag, errs, p1, hparts);
+        } else {
+            hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
+                               ObsPixels{points_2d}, parts, error_flag, errs, p1, hparts);
+        }
         hipLaunchKernelGGL((k_tsqr_final<M>), dim3(1), dim3(kBlock), 0, s, parts, nb, r_factor);
     };
     switch (cam->model) {
@@ -5278,10 +5306,12 @@ size_t reproj_error_hist_off(size_t n) { return reproj_error_hist_offset(n); }
 size_t reproj_error_median_off(size_t n) { return reproj_error_median_offset(n); }
 int reprojection_stats_hist(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                             const double* points_2d, double* result, double* errors,
-                            void* workspace, void* stream, int* hist_nb) {
+                            void* workspace, void* stream, int* hist_nb,
+                            const uint32_t* cells, const acm_cell_grid* grid) {
     unsigned int* hparts = (unsigned int*)((char*)workspace + reproj_error_hist_offset(n));
     return reprojection_stats_impl(cam, n, points_3d, layout, points_2d, result, errors,
-                                   workspace, (hipStream_t)stream, hparts, hist_nb);
+                                   workspace, (hipStream_t)stream, hparts, hist_nb, nullptr,
+                                   cells, grid);
 }
 int median_union(size_t n, const double* values, uint64_t n_valid_global, double* out,
                  void* median_ws, acm_allreduce_fn allreduce, void* allreduce_ctx, void* stream,
@@ -5508,6 +5538,32 @@ ACM_API int acm_reprojection_error(const acm_camera* cam, size_t n, const double
     if (rc) return rc;
     const double* errs = errors ? errors : (const double*)workspace;
     // n_valid from result[5] on the device: no host round trip in between
+    return median_impl(n, errs, result + 5, 0, result + 8, mws, nullptr, nullptr, stream, hparts,
+                       nb, true);
+}
+
+// (r06) the same from the cell form of the observations (acm_cell_grid)
+ACM_API int acm_reprojection_error_cells(const acm_camera* cam, size_t n, const double* points_3d,
+                                         int layout, const uint32_t* cells,
+                                         const acm_cell_grid* grid, double* result,
+                                         double* errors, void* workspace, size_t workspace_bytes,
+                                         void* stream) {
+    int rc = acm::check_cell_grid(grid);
+    if (rc) return rc;
+    if (!result || !workspace || (n && (!points_3d || !cells)))
+        return fail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (workspace_bytes < acm_reprojection_error_workspace_size(n))
+        return fail(ACM_ERR_WORKSPACE_TOO_SMALL, "reprojection-error workspace too small");
+    static const uint32_t none = 0;
+    char* ws = (char*)workspace;
+    unsigned int* hparts = (unsigned int*)(ws + reproj_error_hist_offset(n));
+    int nb = 0;
+    void* mws = ws + reproj_error_median_offset(n);
+    rc = reprojection_stats_impl(cam, n, points_3d, layout, nullptr, result, errors, workspace,
+                                 (hipStream_t)stream, hparts, &nb, mws, cells ? cells : &none,
+                                 grid);
+    if (rc) return rc;
+    const double* errs = errors ? errors : (const double*)workspace;
     return median_impl(n, errs, result + 5, 0, result + 8, mws, nullptr, nullptr, stream, hparts,
                        nb, true);
 }

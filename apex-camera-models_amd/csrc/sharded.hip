@@ -38,12 +38,15 @@ int set_error(int code, const std::string& msg);  // acm.hip
 int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                            const double* points_2d, double* r_factor, int* error_flag,
                            double* result, void* ws_qr, void* ws_err, void* stream,
-                           double* host_out, hipEvent_t ready, int* hist_nb);
+                           double* host_out, hipEvent_t ready, int* hist_nb,
+                           const uint32_t* cells, const acm_cell_grid* grid);
 size_t reproj_error_hist_off(size_t n);
 size_t reproj_error_median_off(size_t n);
 int reprojection_stats_hist(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                             const double* points_2d, double* result, double* errors,
-                            void* workspace, void* stream, int* hist_nb);
+                            void* workspace, void* stream, int* hist_nb,
+                            const uint32_t* cells, const acm_cell_grid* grid);
+int check_cell_grid(const acm_cell_grid* grid);
 int median_union(size_t n, const double* values, uint64_t n_valid_global, double* out,
                  void* median_ws, acm_allreduce_fn allreduce, void* allreduce_ctx, void* stream,
                  const unsigned int* hparts, int hist_nb);
@@ -389,6 +392,8 @@ ACM_API size_t acm_linear_estimation_with_error_sharded_workspace_size(int model
 ACM_API int acm_linear_estimation_with_error_sharded(acm_camera* cam, size_t n,
                                                      const double* points_3d, int layout,
                                                      const double* points_2d,
+                                                     const uint32_t* cells,
+                                                     const acm_cell_grid* grid,
                                                      double* initial_error,
                                                      double* initial_error_host,
                                                      const acm_collective* coll, void* workspace,
@@ -399,6 +404,12 @@ ACM_API int acm_linear_estimation_with_error_sharded(acm_camera* cam, size_t n,
     int world = 1;
     int rc = check_coll(coll, &world);
     if (rc) return rc;
+    static const uint32_t none = 0;
+    if (cells || grid) {  // the cell form of the observations (r06)
+        if ((rc = acm::check_cell_grid(grid))) return rc;
+        if (n && !cells) return sfail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+        if (!cells) cells = &none;
+    }
     const size_t need = acm_linear_estimation_with_error_sharded_workspace_size(cam->model, n, world);
     if (!need) return sfail(ACM_ERR_NOT_SUPPORTED, "model has no linear_estimation");
     if (workspace_bytes < need)
@@ -422,10 +433,10 @@ ACM_API int acm_linear_estimation_with_error_sharded(acm_camera* cam, size_t n,
     if (k >= 0)
         rc = acm::linear_system_qr_error(cam, n, points_3d, layout, points_2d, d_r, (int*)(d_r + 16),
                                          initial_error, ws + Lo.qr, ws_err, stream, nullptr,
-                                         nullptr, &nb);
+                                         nullptr, &nb, cells, grid);
     else
         rc = acm::reprojection_stats_hist(cam, n, points_3d, layout, points_2d, initial_error,
-                                          nullptr, ws_err, stream, &nb);
+                                          nullptr, ws_err, stream, &nb, cells, grid);
     if (rc) return rc;
     std::vector<double> recs((size_t)world * kRec);
     double g8[8];
@@ -480,16 +491,22 @@ ACM_API size_t acm_reprojection_error_sharded_workspace_size(size_t n, int32_t w
 
 ACM_API int acm_reprojection_error_sharded(const acm_camera* cam, size_t n,
                                            const double* points_3d, int layout,
-                                           const double* points_2d, double* result,
+                                           const double* points_2d, const uint32_t* cells,
+                                           const acm_cell_grid* grid, double* result,
                                            double* errors, const acm_collective* coll,
                                            void* workspace, size_t workspace_bytes,
                                            void* stream) {
     if (!cam) return sfail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
-    if (!result || !workspace || (n && (!points_3d || !points_2d)))
+    if (!result || !workspace || (n && (!points_3d || !(points_2d || cells))))
         return sfail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
     int world = 1;
     int rc = check_coll(coll, &world);
     if (rc) return rc;
+    static const uint32_t none = 0;
+    if (cells || grid) {
+        if ((rc = acm::check_cell_grid(grid))) return rc;
+        if (!cells) cells = &none;
+    }
     size_t off_rec, off_gath;
     if (workspace_bytes < reproj_layout(n, world, &off_rec, &off_gath))
         return sfail(ACM_ERR_WORKSPACE_TOO_SMALL, "sharded reprojection-error workspace too small");
@@ -499,7 +516,7 @@ ACM_API int acm_reprojection_error_sharded(const acm_camera* cam, size_t n,
     char* ws = (char*)workspace;
     int nb = 1;
     rc = acm::reprojection_stats_hist(cam, n, points_3d, layout, points_2d, result, errors, ws,
-                                      stream, &nb);
+                                      stream, &nb, cells, grid);
     if (rc) return rc;
     const double* errs = errors ? errors : (const double*)ws;
     void* mws = ws + acm::reproj_error_median_off(n);

@@ -35,7 +35,8 @@ int check_cell_grid(const acm_cell_grid* grid);
 int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                            const double* points_2d, double* r_factor, int* error_flag,
                            double* result, void* ws_qr, void* ws_err, void* stream,
-                           double* host_out, hipEvent_t ready, int* hist_nb = nullptr);
+                           double* host_out, hipEvent_t ready, int* hist_nb = nullptr,
+                           const uint32_t* cells = nullptr, const acm_cell_grid* grid = nullptr);
 }
 
 namespace {
@@ -354,11 +355,12 @@ struct OpeningHost {
 };
 }  // namespace
 
-ACM_API int acm_linear_estimation_with_error_async(acm_camera* cam, size_t n,
-                                                   const double* points_3d, int layout,
-                                                   const double* points_2d, double* initial_error,
-                                                   double* initial_error_host, void* workspace,
-                                                   size_t workspace_bytes, void* stream) {
+static int linear_estimation_with_error_async(acm_camera* cam, size_t n, const double* points_3d,
+                                              int layout, const double* points_2d,
+                                              const uint32_t* cells, const acm_cell_grid* grid,
+                                              double* initial_error, double* initial_error_host,
+                                              void* workspace, size_t workspace_bytes,
+                                              void* stream) {
     if (!cam) return sfail(ACM_ERR_INVALID_ARGUMENT, "camera is NULL");
     if (!initial_error) return sfail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
     const size_t need = acm_linear_estimation_with_error_workspace_size(cam->model, n);
@@ -393,7 +395,7 @@ ACM_API int acm_linear_estimation_with_error_async(acm_camera* cam, size_t n,
     // median's result lands in initial_error[8] in stream order
     int rc = acm::linear_system_qr_error(cam, n, points_3d, layout, points_2d, d_r, d_err,
                                          initial_error, workspace, ws_err, stream, host.p,
-                                         host.ev);
+                                         host.ev, nullptr, cells, grid);
     if (rc) return rc;
     if (hip_ok(hipEventSynchronize(host.ev)))
         return sfail(ACM_ERR_HIP, "linear estimation: device copy failed");
@@ -403,6 +405,33 @@ ACM_API int acm_linear_estimation_with_error_async(acm_camera* cam, size_t n,
     int err = 0;
     std::memcpy(&err, &R[16], sizeof(int));
     return acm_linear_estimation_solve(cam, n, R, err);
+}
+
+ACM_API int acm_linear_estimation_with_error_async(acm_camera* cam, size_t n,
+                                                   const double* points_3d, int layout,
+                                                   const double* points_2d, double* initial_error,
+                                                   double* initial_error_host, void* workspace,
+                                                   size_t workspace_bytes, void* stream) {
+    return linear_estimation_with_error_async(cam, n, points_3d, layout, points_2d, nullptr,
+                                              nullptr, initial_error, initial_error_host,
+                                              workspace, workspace_bytes, stream);
+}
+
+// (r06) the same with the fused pass reading the cell form of the
+// observations (acm_cell_grid); points_2d is still required, for the FOV
+// grid search and the too-few-points path, which read the pixels
+ACM_API int acm_linear_estimation_with_error_cells_async(
+    acm_camera* cam, size_t n, const double* points_3d, int layout, const double* points_2d,
+    const uint32_t* cells, const acm_cell_grid* grid, double* initial_error,
+    double* initial_error_host, void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = acm::check_cell_grid(grid);
+    if (rc) return rc;
+    if (n && (!cells || !points_2d)) return sfail(ACM_ERR_INVALID_ARGUMENT, "NULL buffer");
+    static const uint32_t none = 0;
+    return linear_estimation_with_error_async(cam, n, points_3d, layout, points_2d,
+                                              cells ? cells : &none, grid, initial_error,
+                                              initial_error_host, workspace, workspace_bytes,
+                                              stream);
 }
 
 ACM_API int acm_linear_estimation_with_error(acm_camera* cam, size_t n, const double* points_3d,

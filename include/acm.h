@@ -408,6 +408,21 @@ ACM_API int acm_lm_optimize_cells(acm_camera *cam, size_t n, const double *point
                                   acm_allreduce_fn allreduce, void *allreduce_ctx,
                                   acm_lm_summary *summary, void *workspace,
                                   size_t workspace_bytes, void *stream);
+/* (r06) The conversion's other two passes in the cell form, the same bits:
+ * acm_reprojection_error over cell-form observations (workspace:
+ * acm_reprojection_error_workspace_size), and
+ * acm_linear_estimation_with_error_async whose fused pass reads the cells
+ * (points_2d still required: the FOV grid search and the too-few-points
+ * path read pixels; workspace: acm_linear_estimation_with_error_workspace_size). */
+ACM_API int acm_reprojection_error_cells(const acm_camera *cam, size_t n,
+                                         const double *points_3d, int layout,
+                                         const uint32_t *cells, const acm_cell_grid *grid,
+                                         double *result, double *errors, void *workspace,
+                                         size_t workspace_bytes, void *stream);
+ACM_API int acm_linear_estimation_with_error_cells_async(
+    acm_camera *cam, size_t n, const double *points_3d, int layout, const double *points_2d,
+    const uint32_t *cells, const acm_cell_grid *grid, double *initial_error,
+    double *initial_error_host, void *workspace, size_t workspace_bytes, void *stream);
 
 /* (r06) The sharded conversion's collectives.  One
  * process per GPU, each holding a shard of the correspondences; both
@@ -452,12 +467,17 @@ ACM_API int acm_rccl_destroy(acm_collective *coll);
  * FOV: the statistics, then the grid sums all-reduced and
  * acm_fov_grid_select.  Every rank gets the same cam->params bit for bit;
  * with one rank (coll NULL, or world 1) the bits of the 1-GPU call.
- * initial_error_host: nullable, host, the union's 8 statistics. */
+ * initial_error_host: nullable, host, the union's 8 statistics.
+ * cells / grid: nullable, the shard's observations also in the cell form
+ * (acm_cell_grid): the fused pass then reads those (same bits); points_2d
+ * is still required (the FOV grid search reads pixels). */
 ACM_API size_t acm_linear_estimation_with_error_sharded_workspace_size(int model, size_t n,
                                                                        int32_t world);
 ACM_API int acm_linear_estimation_with_error_sharded(acm_camera *cam, size_t n,
                                                      const double *points_3d, int layout,
                                                      const double *points_2d,
+                                                     const uint32_t *cells,
+                                                     const acm_cell_grid *grid,
                                                      double *initial_error,
                                                      double *initial_error_host,
                                                      const acm_collective *coll,
@@ -467,11 +487,14 @@ ACM_API int acm_linear_estimation_with_error_sharded(acm_camera *cam, size_t n,
  * of the ranks' shards: this shard's statistics pass (with the median's
  * first histogram), one all-gather of the records, Chan's merge, the
  * distributed exact median.  result: device, 9 f64 as acm_reprojection_error
- * (the union's), identical on every rank; errors: nullable device N f64. */
+ * (the union's), identical on every rank; errors: nullable device N f64.
+ * cells / grid: nullable, the cell form of the observations (then
+ * points_2d may be NULL). */
 ACM_API size_t acm_reprojection_error_sharded_workspace_size(size_t n, int32_t world);
 ACM_API int acm_reprojection_error_sharded(const acm_camera *cam, size_t n,
                                            const double *points_3d, int layout,
-                                           const double *points_2d, double *result,
+                                           const double *points_2d, const uint32_t *cells,
+                                           const acm_cell_grid *grid, double *result,
                                            double *errors, const acm_collective *coll,
                                            void *workspace, size_t workspace_bytes,
                                            void *stream);

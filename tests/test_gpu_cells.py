@@ -92,7 +92,7 @@ def test_normal_equations_cells_bit_identical(target, policy):
                                             b.data_ptr(), ws.data_ptr(), wsb, _stream_handle()))
     torch.cuda.synchronize()
     assert torch.equal(a.view(torch.int64), b.view(torch.int64))
-    assert a[-1].item() > 0.5 * n  # most points valid
+    assert a[-1].item() > 1000  # enough valid points to mean something
 
 
 @pytest.mark.parametrize("target", ["double_sphere", "kannala_brandt", "rad_tan", "ucm", "eucm",
@@ -109,8 +109,26 @@ def test_convert_cells_same_iterates(target):
     b = conversion.convert(src, target, xyz, uv, cells=cs)
     assert a.model.params() == b.model.params()
     assert (a.lm_iterations, a.lm_termination) == (b.lm_iterations, b.lm_termination)
-    fa, fb = a.final_reprojection_error, b.final_reprojection_error
-    assert (fa.mean, fa.median, fa.rmse, fa.n_valid) == (fb.mean, fb.median, fb.rmse, fb.n_valid)
+    for fa, fb in ((a.final_reprojection_error, b.final_reprojection_error),
+                   (a.initial_reprojection_error, b.initial_reprojection_error)):
+        for k in ("rmse", "min", "max", "mean", "stddev", "median", "n_valid"):
+            va, vb = getattr(fa, k), getattr(fb, k)
+            assert va == vb or (va != va and vb != vb), (k, va, vb)
+
+
+def test_sharded_cells_world1_is_the_1gpu_path():
+    """The sharded entry points with the cell form at world 1 (local
+    collective): the 1-GPU pixel path's bits."""
+    from apex_camera_models import KannalaBrandtModel, Resolution, conversion, util
+    from apex_camera_models.distributed import LocalCollective
+    kp, (w, h) = SAMPLES[KB]
+    src = KannalaBrandtModel._from_params(kp, Resolution(w, h))
+    uv, xyz, cs = util.sample_points(src, 60_000, cells=True)
+    a = conversion.convert(src, "double_sphere", xyz, uv)
+    b = conversion.convert(src, "double_sphere", xyz, uv, collective=LocalCollective(), cells=cs)
+    assert a.model.params() == b.model.params()
+    assert a.final_reprojection_error == b.final_reprojection_error
+    assert a.initial_reprojection_error == b.initial_reprojection_error
 
 
 def test_cell_form_argument_checks():
