@@ -123,7 +123,8 @@ def test_sharded_reprojection_error_matches_unsharded():
     r2 = torch.empty(9, dtype=torch.float64, device="cuda")
     e2 = torch.empty(n, dtype=torch.float64, device="cuda")
     _lib.check(L.acm_reprojection_error_sharded(ctypes.byref(cam), n, p3.data_ptr(), 0,
-                                                p2.data_ptr(), r2.data_ptr(), e2.data_ptr(),
+                                                p2.data_ptr(), None, None, r2.data_ptr(),
+                                                e2.data_ptr(),
                                                 ctypes.byref(coll.c), ws2.data_ptr(), nb,
                                                 _stream_handle()))
     torch.cuda.synchronize()
@@ -153,7 +154,8 @@ def test_sharded_opening_counts_the_union():
     host = (ctypes.c_double * 8)()
     cam = m.acm_camera()
     rc = L.acm_linear_estimation_with_error_sharded(ctypes.byref(cam), 3, xyz.data_ptr(), 0,
-                                                    uv.data_ptr(), res.data_ptr(), host,
+                                                    uv.data_ptr(), None, None, res.data_ptr(),
+                                                    host,
                                                     ctypes.byref(coll.c), ws.data_ptr(), nb,
                                                     _stream_handle())
     assert rc == _lib.ERR_INVALID_PARAMS
