@@ -1148,11 +1148,10 @@ struct ObsCells {
 // (amdgpu_waves_per_eu).  1 leaves it free (KB lands at 176 VGPRs = 2 waves);
 // 3 fits KB in 168 without spills; 4 forces 128 with scratch spills for KB and
 // RadTan.  Selected per launch by ACM_TUNE_NE_WAVES (results identical).
-template <class TagT, int LAYOUT, int WAVES, int U, bool NTL, class OBS = ObsPixels>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq(acm_camera cam, size_t n,
-                                                      const double* __restrict__ pts,
-                                                      OBS obs, int policy,
-                                                      double* __restrict__ parts) {
+template <class TagT, int LAYOUT, int U, bool NTL, class OBS>
+__device__ __forceinline__ void normal_eq_body(const acm_camera& cam, size_t n,
+                                               const double* __restrict__ pts, OBS obs,
+                                               int policy, double* __restrict__ parts) {
     using ORaw = typename OBS::raw;
     using Acc = NeAccum<TagT>;
     constexpr int K = Acc::K;
@@ -1260,6 +1259,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         }
     }
     sums.store(parts + blockIdx.x, gridDim.x);
+}
+template <class TagT, int LAYOUT, int WAVES, int U, bool NTL, class OBS = ObsPixels>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq(acm_camera cam, size_t n,
+                                                      const double* __restrict__ pts,
+                                                      OBS obs, int policy,
+                                                      double* __restrict__ parts) {
+    normal_eq_body<TagT, LAYOUT, U, NTL, OBS>(cam, n, pts, obs, policy, parts);
+}
+// (r06) The LM's pre-queued evaluation (solver.hip, ACM_TUNE_LM_HOST_RESULT
+// 3): the camera is read from device memory, where the one-wave doorbell
+// kernel queued ahead of this one copied it from the host's mailbox; a
+// negative model there means the evaluation was cancelled (or its doorbell
+// timed out) and nothing is computed.  The same body, so the same sums.
+template <class TagT, int LAYOUT, int WAVES, int U, bool NTL, class OBS = ObsPixels>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq_dev(
+        const acm_camera* __restrict__ camp, size_t n, const double* __restrict__ pts, OBS obs,
+        int policy, double* __restrict__ parts) {
+    const acm_camera cam = *camp;
+    if (cam.model < 0) return;
+    normal_eq_body<TagT, LAYOUT, U, NTL, OBS>(cam, n, pts, obs, policy, parts);
 }
 
 // Epilogue of k_normal_eq: sum the per-workgroup partials (nb x K,
@@ -4578,12 +4597,19 @@ static ObsCells obs_cells(const uint32_t* cells, const acm_cell_grid& g) {
     o.ch = (double)g.height / (double)g.num_cells_y;  // acm_sample_points_ex computes them
     return o;
 }
+// (r06) whether normal_equations_impl can run the pre-queued evaluation
+// (k_normal_eq_dev, instantiated for the default configuration only): AoS
+// points, the default waves / unroll knobs and NT loads on
+bool ne_dev_ok(int layout) {
+    return layout == ACM_LAYOUT_AOS && g_nt_loads != 0 && g_ne_waves == 0 && g_ne_unroll == 0;
+}
+
 int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                           const double* points_2d_obs, int invalid_policy, double* result,
                           void* workspace, size_t workspace_bytes, void* stream,
                           unsigned long long* flag, unsigned long long seq,
                           unsigned int* ticket, const uint32_t* cells,
-                          const acm_cell_grid* grid) {
+                          const acm_cell_grid* grid, const acm_camera* dev_cam) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -4619,6 +4645,13 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
                             : k_normal_eq<TagT, LAY, Def::W, Def::U, false, ObsPixels>;
             const int cap = resident_blocks(reinterpret_cast<const void*>(kpix));
             if (nb > cap) nb = cap;
+            if (dev_cam) {  // (r06) the pre-queued LM evaluation: AoS, NT loads (ne_dev_ok)
+                hipLaunchKernelGGL((k_normal_eq_dev<TagT, ACM_LAYOUT_AOS, Def::W, Def::U, true,
+                                                    ObsCells>),
+                                   dim3(nb), dim3(kBlock), 0, s, dev_cam, n, points_3d,
+                                   obs_cells(cells, *grid), invalid_policy, parts);
+                return;
+            }
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
                                obs_cells(cells, *grid), invalid_policy, parts);
         };
@@ -4637,10 +4670,22 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
             }
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
+            if (dev_cam) {  // (ne_dev_ok: the default W, U; AoS; NT loads)
+                hipLaunchKernelGGL((k_normal_eq_dev<TagT, ACM_LAYOUT_AOS, Def::W, Def::U, true>),
+                                   dim3(nb), dim3(kBlock), 0, s, dev_cam, n, points_3d,
+                                   ObsPixels{points_2d_obs}, invalid_policy, parts);
+                return;
+            }
             hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, s, prep(*cam), n, points_3d,
                                ObsPixels{points_2d_obs}, invalid_policy, parts);
         };
         auto by_waves = [&](auto lay_c) {
+            if (dev_cam) {  // the default kernel's partition (nb), then the dev form
+                if constexpr (Def::W == 1) go(lay_c, std::integral_constant<int, 1>{});
+                else if constexpr (Def::W == 4) go(lay_c, std::integral_constant<int, 4>{});
+                else go(lay_c, std::integral_constant<int, 3>{});
+                return;
+            }
             switch (wv) {
             case 1: go(lay_c, std::integral_constant<int, 1>{}); break;
             case 4: go(lay_c, std::integral_constant<int, 4>{}); break;
@@ -4681,7 +4726,7 @@ ACM_API int acm_normal_equations(const acm_camera* cam, size_t n, const double* 
                                  void* stream) {
     return acm::normal_equations_impl(cam, n, points_3d, layout, points_2d_obs, invalid_policy,
                                       result, workspace, workspace_bytes, stream, nullptr, 0,
-                                      nullptr, nullptr, nullptr);
+                                      nullptr, nullptr, nullptr, nullptr);
 }
 
 ACM_API int acm_normal_equations_cells(const acm_camera* cam, size_t n, const double* points_3d,
@@ -4696,7 +4741,7 @@ ACM_API int acm_normal_equations_cells(const acm_camera* cam, size_t n, const do
     }
     return acm::normal_equations_impl(cam, n, points_3d, layout, nullptr, invalid_policy,
                                       result, workspace, workspace_bytes, stream, nullptr, 0,
-                                      nullptr, cells, grid);
+                                      nullptr, cells, grid, nullptr);
 }
 
 ACM_API size_t acm_reprojection_stats_workspace_size(size_t n) {
@@ -5649,7 +5694,7 @@ ACM_API int acm_set_tuning(int key, int value) {
         {ACM_TUNE_ALIGN_J, &g_align_j, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NT_LOADS, &g_nt_loads, -1, 1, "value must be -1..1"},
         {ACM_TUNE_NT_LOADS_UNPROJECT, &g_nt_loads_unproject, -1, 1, "value must be -1..1"},
-        {ACM_TUNE_LM_HOST_RESULT, &g_lm_host_result, -1, 2, "value must be -1..2"},
+        {ACM_TUNE_LM_HOST_RESULT, &g_lm_host_result, -1, 3, "value must be -1..3"},
         {ACM_TUNE_SAMPLE_FUSED, &g_sample_fused, -1, 4, "value must be -1..4"},
         {ACM_TUNE_UNPROJECT_RCP, &g_unproject_rcp, -1, 1, "value must be -1..1"},
         {ACM_TUNE_SAMPLE_PATIENCE, &g_sample_patience, -1, 1 << 20, "value must be -1..2^20"},

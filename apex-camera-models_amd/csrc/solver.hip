@@ -30,7 +30,8 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
                           void* workspace, size_t workspace_bytes, void* stream,
                           unsigned long long* flag, unsigned long long seq,
                           unsigned int* ticket, const uint32_t* cells,
-                          const acm_cell_grid* grid);
+                          const acm_cell_grid* grid, const acm_camera* dev_cam);
+bool ne_dev_ok(int layout);
 int check_cell_grid(const acm_cell_grid* grid);
 int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
                            const double* points_2d, double* r_factor, int* error_flag,
@@ -459,6 +460,59 @@ __global__ void k_lm_copy_publish(const double* __restrict__ src, double* __rest
     }
 }
 
+// (r06) The doorbell of the pre-queued LM evaluation (ACM_TUNE_LM_HOST_RESULT
+// 3).  The host queues [k_lm_doorbell | normal equations from the device
+// camera | epilogue] for evaluation k + 1 while evaluation k runs; when k's
+// results are in and the LM wants another point, the host writes the camera
+// into the mailbox and then the sequence number, and the evaluation is
+// already on the GPU: no launch between the host's decision and the kernel.
+// Mailbox: pinned, coherent host memory.
+struct LmMailbox {
+    unsigned long long seq;  // host: written last (release)
+    unsigned long long ack;  // k_lm_doorbell: seq when served, else seq | kLmNotServed
+    acm_camera cam;          // host: the parameters to evaluate
+};
+constexpr unsigned long long kLmCancel = 1ull << 62;     // host: no evaluation after all
+constexpr unsigned long long kLmNotServed = 1ull << 63;  // device: cancelled or timed out
+
+// One wave: every lane polls the sequence word (one request), with a bounded
+// wait (timeout_ticks of the constant-rate wall clock) so the grid always
+// drains; then copies the camera (22 dwords) to device memory with vector
+// stores, or marks it cancelled (model = -1) for the evaluation queued behind.
+__global__ __launch_bounds__(64) void k_lm_doorbell(const LmMailbox* mb, unsigned long long seq,
+                                                    acm_camera* __restrict__ dst,
+                                                    unsigned long long* ack,
+                                                    unsigned long long timeout_ticks) {
+    const unsigned long long t0 = wall_clock64();
+    bool served = false;
+    for (;;) {
+        const unsigned long long v =
+            __hip_atomic_load(&mb->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+        const unsigned long long u = ((unsigned long long)hi << 32) | lo;
+        if (u == seq) {
+            served = true;
+            break;
+        }
+        if (u == (seq | kLmCancel) || wall_clock64() - t0 > timeout_ticks) break;
+        __builtin_amdgcn_s_sleep(8);
+    }
+    constexpr int kWords = (int)(sizeof(acm_camera) / 4);
+    const unsigned lane = threadIdx.x;
+    if (served) {
+        if (lane < kWords)
+            reinterpret_cast<unsigned*>(dst)[lane] =
+                __hip_atomic_load(reinterpret_cast<const unsigned*>(&mb->cam) + lane,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (lane == 0) {
+        dst->model = -1;
+    }
+    if (lane == 0)
+        __hip_atomic_store(ack, served ? seq : (seq | kLmNotServed), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 ACM_API void acm_lm_default_config(acm_lm_config* cfg) {
     if (!cfg) return;
     std::memset(cfg, 0, sizeof(*cfg));
@@ -476,11 +530,149 @@ ACM_API void acm_lm_default_config(acm_lm_config* cfg) {
 }
 
 // LM workspace: the normal equations' partials | the results (R doubles + 8
-// spare, one of them the finish kernel's ticket).
+// spare, one of them the finish kernel's ticket) | (r06) the pre-queued
+// evaluation's camera (12 doubles).
+constexpr int kLmDevCamDoubles = (int)((sizeof(acm_camera) + 7) / 8);
 ACM_API size_t acm_lm_workspace_size(int model, size_t n) {
     const int P = acm_num_params(model);
     if (P < 0) return 0;
-    return acm_normal_equations_workspace_size(model, n) + (size_t)(P * P + P + 2 + 8) * 8;
+    return acm_normal_equations_workspace_size(model, n) +
+           (size_t)(P * P + P + 2 + 8 + kLmDevCamDoubles) * 8;
+}
+
+static void lm_summarize(const acm::lm::State& st, acm_camera* cam, int P,
+                         acm_lm_summary* summary) {
+    for (int i = 0; i < P; ++i) cam->params[i] = st.x[i];
+    acm_lm_summary sum;
+    std::memset(&sum, 0, sizeof(sum));
+    sum.iterations = st.it;
+    sum.termination = st.term;
+    sum.evaluations = st.evals;
+    sum.initial_cost = st.initial_cost;
+    sum.final_cost = st.F;
+    sum.n_valid = st.nv;
+    if (summary) *summary = sum;
+}
+
+// (r06) The LM host loop with pre-queued evaluations (ACM_TUNE_LM_HOST_RESULT
+// 3; k_lm_doorbell above).  The same evaluations in the same order as the
+// launch-per-evaluation loop, from the same kernel body: the same iterates.
+static int lm_doorbell_loop(acm_camera* cam, size_t n, const double* points_3d, int layout,
+                            const double* points_2d, const uint32_t* cells,
+                            const acm_cell_grid* grid, const acm_lm_config* cfg,
+                            acm::lm::State& st, int P, double* pinned, unsigned long long& seq,
+                            double* d_res, void* workspace, size_t ne_ws,
+                            acm_lm_summary* summary, hipStream_t s) {
+    struct Mailbox {
+        LmMailbox* p = nullptr;
+        ~Mailbox() {
+            if (p && hipHostFree(p) != hipSuccess) (void)hipGetLastError();
+        }
+    };
+    static thread_local Mailbox tl_mb;
+    if (!tl_mb.p) {
+        void* q = nullptr;
+        if (hipHostMalloc(&q, 4096, hipHostMallocMapped | hipHostMallocPortable |
+                                        hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            return sfail(ACM_ERR_HIP, "LM: mailbox allocation failed");
+        }
+        tl_mb.p = (LmMailbox*)q;
+        std::memset(q, 0, 4096);
+    }
+    LmMailbox* mb = tl_mb.p;
+    int dev = 0, khz = 0;
+    if (hip_ok(hipGetDevice(&dev)) ||
+        hip_ok(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev)) || khz <= 0)
+        return sfail(ACM_ERR_HIP, "LM: wall clock rate unavailable");
+    // a doorbell not rung within 10 s ends its wait (the evaluation is then
+    // reported as failed): the queued kernels always drain
+    const unsigned long long timeout = 10000ull * (unsigned long long)khz;
+    const int R = P * P + P + 2;
+    auto* flag = reinterpret_cast<unsigned long long*>(pinned + 127);
+    auto* ticket = reinterpret_cast<unsigned int*>(d_res + R);
+    auto* dev_cam = reinterpret_cast<acm_camera*>(d_res + R + 8);
+    auto* ack = &mb->ack;
+    if (hip_ok(hipMemsetAsync(ticket, 0, sizeof(unsigned int), s)))
+        return sfail(ACM_ERR_HIP, "LM: ticket reset failed");
+    // queue evaluation `q`: the doorbell wait, then the normal equations and
+    // their epilogue (results into the pinned buffer, completion word = q)
+    auto enqueue = [&](unsigned long long q) -> int {
+        hipLaunchKernelGGL(k_lm_doorbell, dim3(1), dim3(64), 0, s, mb, q, dev_cam, ack, timeout);
+        if (hip_ok(hipGetLastError())) return sfail(ACM_ERR_HIP, "LM: doorbell launch");
+        return acm::normal_equations_impl(cam, n, points_3d, layout, points_2d,
+                                          cfg->invalid_policy, pinned, workspace, ne_ws, s, flag,
+                                          q, ticket, cells, grid, dev_cam);
+    };
+    auto ring = [&](unsigned long long q, const double* x) {
+        acm_camera c = *cam;
+        for (int i = 0; i < P; ++i) c.params[i] = x[i];
+        std::memcpy(&mb->cam, &c, sizeof(c));
+        __atomic_store_n(&mb->seq, q, __ATOMIC_RELEASE);
+    };
+    // spin on evaluation q's completion word (as the mode-2 loop), then
+    // check that its doorbell served it
+    auto wait = [&](unsigned long long q) -> int {
+        for (unsigned spin = 1;; ++spin) {
+            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == q) break;
+            if ((spin & 255) == 0) {
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipSuccess) {
+                    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == q) break;
+                    return sfail(ACM_ERR_HIP, "LM: completion word not published");
+                }
+                if (e != hipErrorNotReady) return sfail(ACM_ERR_HIP, "LM: stream failed");
+            }
+            __builtin_ia32_pause();
+        }
+        return ACM_SUCCESS;
+    };
+    // a queued evaluation the loop no longer wants: cancel it and let the
+    // queue drain before returning (its epilogue still publishes q)
+    auto cancel = [&](unsigned long long q) {
+        __atomic_store_n(&mb->seq, q | kLmCancel, __ATOMIC_RELEASE);
+        (void)wait(q);
+    };
+    // on an error: cancel q (perhaps only partly queued) and drain the stream
+    auto abandon = [&](unsigned long long q) {
+        __atomic_store_n(&mb->seq, q | kLmCancel, __ATOMIC_RELEASE);
+        if (hipStreamSynchronize(s) != hipSuccess) (void)hipGetLastError();
+    };
+    std::vector<double> res(R);
+    unsigned long long cur = ++seq;
+    int rc = enqueue(cur);
+    if (rc) {
+        abandon(cur);
+        return rc;
+    }
+    ring(cur, st.xn);
+    int r = acm::lm::NEED_EVAL;
+    while (r == acm::lm::NEED_EVAL) {
+        const unsigned long long next = ++seq;
+        if ((rc = enqueue(next))) {
+            (void)wait(cur);
+            abandon(next);
+            return rc;
+        }
+        if ((rc = wait(cur))) {
+            abandon(next);
+            return rc;
+        }
+        if (__atomic_load_n(ack, __ATOMIC_ACQUIRE) != cur) {
+            cancel(next);
+            return sfail(ACM_ERR_HIP, "LM: evaluation not served (doorbell timed out)");
+        }
+        std::memcpy(res.data(), pinned, R * sizeof(double));
+        r = acm::lm::consume(st, *cfg, res.data(), P);
+        if (r != acm::lm::NEED_EVAL) {
+            cancel(next);
+            break;
+        }
+        ring(next, st.xn);
+        cur = next;
+    }
+    lm_summarize(st, cam, P, summary);
+    return ACM_SUCCESS;
 }
 
 static int lm_optimize(acm_camera* cam, size_t n, const double* points_3d, int layout,
@@ -530,7 +722,11 @@ static int lm_optimize(acm_camera* cam, size_t n, const double* points_3d, int l
         else
             (void)hipGetLastError();
     }
-    const int host_mode = pinned ? knob : 0;
+    int host_mode = pinned ? knob : 0;
+    // (r06) 3: the pre-queued evaluations (lm_doorbell_loop) where the
+    // normal equations support them, else the mode-2 loop
+    const bool doorbell = host_mode == 3 && !allreduce && acm::ne_dev_ok(layout);
+    if (host_mode == 3) host_mode = 2;
     double* res_out = d_res;
     unsigned long long* flag = nullptr;
     // the finish kernel's ticket (mode 2 without an all-reduce): one of
@@ -554,7 +750,8 @@ static int lm_optimize(acm_camera* cam, size_t n, const double* points_3d, int l
         const unsigned long long want = flag ? ++seq : 0;
         int rc = acm::normal_equations_impl(&c, n, points_3d, layout, points_2d,
                                             cfg->invalid_policy, res_out, workspace, ne_ws, stream,
-                                            allreduce ? nullptr : flag, want, ticket, cells, grid);
+                                            allreduce ? nullptr : flag, want, ticket, cells, grid,
+                                            nullptr);
         if (rc) return rc;
         if (allreduce) {
             rc = allreduce(allreduce_ctx, d_res, (size_t)R, stream);
@@ -598,6 +795,10 @@ static int lm_optimize(acm_camera* cam, size_t n, const double* points_3d, int l
 
     acm::lm::State st;
     acm::lm::start(st, *cfg, P, cam->params);
+    if (doorbell) {
+        return lm_doorbell_loop(cam, n, points_3d, layout, points_2d, cells, grid, cfg, st, P,
+                                pinned, seq, d_res, workspace, ne_ws, summary, s);
+    }
     // the host loop: one normal-equations evaluation per state-machine step
     // (lm_core.hpp).  A device-resident form of this loop (r04: the state
     // machine in a one-wave kernel behind each evaluation, the host queueing
@@ -610,16 +811,7 @@ static int lm_optimize(acm_camera* cam, size_t n, const double* points_3d, int l
         if (rc) return rc;
         r = acm::lm::consume(st, *cfg, res.data(), P);
     }
-    for (int i = 0; i < P; ++i) cam->params[i] = st.x[i];
-    acm_lm_summary sum;
-    std::memset(&sum, 0, sizeof(sum));
-    sum.iterations = st.it;
-    sum.termination = st.term;
-    sum.evaluations = st.evals;
-    sum.initial_cost = st.initial_cost;
-    sum.final_cost = st.F;
-    sum.n_valid = st.nv;
-    if (summary) *summary = sum;
+    lm_summarize(st, cam, P, summary);
     return ACM_SUCCESS;
 }
 

@@ -158,7 +158,7 @@ def test_tuning_knobs_validate_and_restore():
              _lib.TUNE_ALIGN_J: ([-1, 0, 1], [2]),
              _lib.TUNE_NT_LOADS: ([-1, 0, 1], [2]),
              _lib.TUNE_NT_LOADS_UNPROJECT: ([-1, 0, 1], [2]),
-             _lib.TUNE_LM_HOST_RESULT: ([-1, 0, 1, 2], [3, -2]),
+             _lib.TUNE_LM_HOST_RESULT: ([-1, 0, 1, 2, 3], [4, -2]),
              _lib.TUNE_SAMPLE_FUSED: ([-1, 0, 1, 2, 3, 4], [5, -2]),
              _lib.TUNE_UNPROJECT_RCP: ([-1, 0, 1], [2, -2]),
              _lib.TUNE_SAMPLE_CERT: ([-1, 0], [1, -2]),

@@ -218,7 +218,7 @@ def test_lm_host_result_matches_device_copy():
     uv, xyz = util.sample_points(src, 200_000)
     runs = []
     try:
-        for v in (0, 1, 2):
+        for v in (0, 1, 2, 3):
             L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, v)
             runs.append(conversion.convert(src, "double_sphere", xyz, uv))
     finally:
@@ -233,9 +233,10 @@ def test_lm_host_result_matches_device_copy():
 def test_lm_host_result_modes_bit_identical(target):
     """The LM takes the same iterates, bit for bit -- parameters, iterations,
     evaluations, termination and both costs -- with each result mode of the
-    host loop (ACM_TUNE_LM_HOST_RESULT 2 / 1 / 0), on a ragged correspondence
-    count; a DS source exercises KB as the target (the LM from a perturbed
-    start).  (r04's device-resident loop, removed in r05, was checked here
+    host loop (ACM_TUNE_LM_HOST_RESULT 2 / 1 / 0, and r06's
+    3: evaluations queued ahead behind a host-written doorbell, also on the
+    cell form), on a ragged correspondence count; a DS source exercises KB as
+    the target (the LM from a perturbed start).  (r04's device-resident loop, removed in r05, was checked here
     against the same runs.)"""
     from apex_camera_models import (DoubleSphereModel, KannalaBrandtModel, Resolution, _lib,
                                     conversion, util)
@@ -249,22 +250,23 @@ def test_lm_host_result_modes_bit_identical(target):
         p, (w, h) = SAMPLES[KB]
         src = KannalaBrandtModel._from_params(p, Resolution(w, h))
         tgt = target
-    uv, xyz = util.sample_points(src, 300_001)
+    uv, xyz, cs = util.sample_points(src, 300_001, cells=True)
     init = conversion._init_target(tgt, src)
     init.linear_estimation(xyz, uv)
     p0 = init.params()
     runs = {}
     try:
-        for host in (2, 1, 0):
+        for host, cells in ((2, None), (1, None), (0, None), (3, None), (3, cs), (2, cs)):
             L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, host)
             m = conversion._init_target(tgt, src)
             m._set_params(list(p0))
-            r = LevenbergMarquardt().optimize(m, xyz, uv, bounds=CONVERTER_BOUNDS[tgt])
-            runs[host] = (m.params(), r.iterations, r.evaluations, r.termination,
-                          r.initial_cost, r.final_cost)
+            r = LevenbergMarquardt().optimize(m, xyz, uv, bounds=CONVERTER_BOUNDS[tgt],
+                                              cells=cells)
+            runs[(host, cells is not None)] = (m.params(), r.iterations, r.evaluations,
+                                               r.termination, r.initial_cost, r.final_cost)
     finally:
         L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, -1)
-    ref = runs[2]
+    ref = runs[(2, False)]
     assert ref[1] >= 1 and ref[2] >= 2, ref
     for k, r in runs.items():
         assert r == ref, (k, r, ref)
@@ -273,21 +275,28 @@ def test_lm_host_result_modes_bit_identical(target):
 def test_lm_iteration_caps():
     """max_iterations caps (0, 1, 2, 5): a run cut short by the cap ends
     with MaxIterations after cap + 1 evaluations (the start point's and one
-    per iteration); the same cap twice gives the same run."""
-    from apex_camera_models import KannalaBrandtModel, Resolution, conversion, util
+    per iteration); the same cap twice gives the same run, and so does the
+    doorbell loop (ACM_TUNE_LM_HOST_RESULT 3), whose queued-ahead evaluation
+    is cancelled at every stop."""
+    from apex_camera_models import KannalaBrandtModel, Resolution, _lib, conversion, util
     from apex_camera_models.optimizer import (CONVERTER_BOUNDS, LevenbergMarquardt,
                                               LevenbergMarquardtConfig)
+    L = _lib.load()
     p, (w, h) = SAMPLES[KB]
     src = KannalaBrandtModel._from_params(p, Resolution(w, h))
     uv, xyz = util.sample_points(src, 50_000)
     for cap in (0, 1, 2, 5):
         got = []
-        for _ in range(2):
-            m = conversion._init_target("double_sphere", src)
-            r = LevenbergMarquardt(LevenbergMarquardtConfig().with_max_iterations(cap)) \
-                .optimize(m, xyz, uv, bounds=CONVERTER_BOUNDS["double_sphere"])
-            got.append((m.params(), r.iterations, r.evaluations, r.termination))
-        assert got[0] == got[1], (cap, got)
+        try:
+            for host in (2, 2, 3, 3):
+                L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, host)
+                m = conversion._init_target("double_sphere", src)
+                r = LevenbergMarquardt(LevenbergMarquardtConfig().with_max_iterations(cap)) \
+                    .optimize(m, xyz, uv, bounds=CONVERTER_BOUNDS["double_sphere"])
+                got.append((m.params(), r.iterations, r.evaluations, r.termination))
+        finally:
+            L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, -1)
+        assert all(g == got[0] for g in got), (cap, got)
         assert got[0][1] <= cap
         assert got[0][2] == min(cap, got[0][1]) + 1 or got[0][3] != "MaxIterations"
 

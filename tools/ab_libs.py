@@ -94,6 +94,17 @@ def main():
                                                    uv.data_ptr(), st.data_ptr(),
                                                    rays.data_ptr(), st2.data_ptr(), sh)
         timed_ab(f"round_trip_{nm}", m, 66, make)
+        # every library's outputs, bit for bit (a timing A/B of two builds
+        # that must not change results)
+        outs = []
+        for tag, L in libs:
+            make(L)()
+            torch.cuda.synchronize()
+            outs.append((tag, [t.clone() for t in (uv, st, rays, st2)]))
+        same = all(torch.equal(x.view(torch.uint8), y.view(torch.uint8))
+                   for _, o in outs[1:] for x, y in zip(outs[0][1], o))
+        print(json.dumps({"call": f"round_trip_{nm}", "same_bits": same}), flush=True)
+        del outs
     del pts, uv, st, rays, st2
     n = a.points
     pts = samples.synthetic_points_device(n)

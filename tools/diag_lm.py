@@ -2,7 +2,9 @@
 wall time of acm_lm_optimize vs evaluations x the normal-equation kernel
 time, i.e. the host / launch / copy cost per evaluation, for the host loop
 with each ACM_TUNE_LM_HOST_RESULT mode (0 copy + sync, 1 pinned + sync, 2
-pinned + spin on the completion word); the reported wall is the default (2).
+pinned + spin on the completion word, 3 (r06) pre-queued evaluations behind a
+host-written doorbell); the reported wall is the default.  Every mode must
+take the same iterates (same parameters bit for bit).
 (r04 also timed a device-resident loop here; it was removed in r05.)
 
   python tools/diag_lm.py [--points N]
@@ -50,7 +52,8 @@ def main():
     L = _lib.load()
     by_mode = {}
     res = None
-    modes = {"host0": 0, "host1": 1, "host2": 2}
+    modes = {"host0": 0, "host1": 1, "host2": 2, "host3": 3}
+    params = {}
     for _ in range(3):
         for mode, host in modes.items():
             L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, host)
@@ -63,14 +66,20 @@ def main():
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3
             by_mode[mode] = min(by_mode.get(mode, 1e9), ms)
+            params[mode] = (tuple(res.parameters), res.evaluations, res.termination)
     L.acm_set_tuning(_lib.TUNE_LM_HOST_RESULT, -1)
-    wall = by_mode["host2"]
+    default = "host2"  # lm_host_result() for -1 (csrc/acm.hip)
+    wall = by_mode[default]
+    ref = params["host2"]
     print(json.dumps({"what": "LM loop overhead", "points": n, "lm_wall_ms": round(wall, 3),
+                      "default_mode": default,
                       "lm_wall_ms_by_mode": {k: round(v, 3) for k, v in by_mode.items()},
+                      "same_iterates_as_host2": {k: v == ref for k, v in params.items()},
                       "evaluations": res.evaluations, "iterations": res.iterations,
                       "ne_ms": round(ne_ms, 4),
-                      "overhead_per_eval_ms": round((wall - res.evaluations * ne_ms)
-                                                    / res.evaluations, 4)}))
+                      "overhead_per_eval_ms": {k: round((v - res.evaluations * ne_ms)
+                                                        / res.evaluations, 4)
+                                               for k, v in by_mode.items()}}))
 
 
 if __name__ == "__main__":
