@@ -31,6 +31,7 @@
 
 #include "acm.h"
 #include "camera_models.hpp"
+#include "lm_doorbell.hpp"
 
 namespace acm {
 
@@ -751,7 +752,7 @@ template <> struct UnprojectStaged<Tag<RadTan>> { static constexpr bool on = fal
 
 // acm_project_unproject's defaults per model: points per lane and whether
 // the AoS rays go out LDS-staged (ACM_TUNE_ROUND_TRIP overrides both).
-// From the r05 A/B at config 4's 50M points (tools/diag_round_trip.py,
+// From the r05 A/B at config 4's 50M points (tools/probes.py round_trip,
 // profiles/r05d_round_trip_ab.log, best of 3 interleaved blocks): one point
 // per lane for Pinhole / UCM / EUCM (0.565 -> 0.553 ms) and for KB, whose
 // rays are now staged too (its VALU work fell with the SGPR-spill fix:
@@ -1268,16 +1269,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     normal_eq_body<TagT, LAYOUT, U, NTL, OBS>(cam, n, pts, obs, policy, parts);
 }
 // (r06) The LM's pre-queued evaluation (solver.hip, ACM_TUNE_LM_HOST_RESULT
-// 3): the camera is read from device memory, where the one-wave doorbell
-// kernel queued ahead of this one copied it from the host's mailbox; a
-// negative model there means the evaluation was cancelled (or its doorbell
-// timed out) and nothing is computed.  The same body, so the same sums.
+// 3): queued while the previous evaluation runs, it waits for the host's
+// doorbell (lm_doorbell.hpp) and reads the camera the doorbell delivered.
+// The same body, so the same sums; a cancelled evaluation computes nothing.
 template <class TagT, int LAYOUT, int WAVES, int U, bool NTL, class OBS = ObsPixels>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_normal_eq_dev(
-        const acm_camera* __restrict__ camp, size_t n, const double* __restrict__ pts, OBS obs,
-        int policy, double* __restrict__ parts) {
-    const acm_camera cam = *camp;
-    if (cam.model < 0) return;
+        LmDoorbell db, size_t n, const double* __restrict__ pts, OBS obs, int policy,
+        double* __restrict__ parts) {
+    if (!lm_doorbell_wait(db)) return;
+    const acm_camera cam = lm_doorbell_camera(db.cam);
     normal_eq_body<TagT, LAYOUT, U, NTL, OBS>(cam, n, pts, obs, policy, parts);
 }
 
@@ -4609,7 +4609,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
                           void* workspace, size_t workspace_bytes, void* stream,
                           unsigned long long* flag, unsigned long long seq,
                           unsigned int* ticket, const uint32_t* cells,
-                          const acm_cell_grid* grid, const acm_camera* dev_cam) {
+                          const acm_cell_grid* grid, const LmDoorbell* db) {
     int rc = check_cam(cam);
     if (rc) return rc;
     if ((rc = check_layout(layout))) return rc;
@@ -4645,10 +4645,10 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
                             : k_normal_eq<TagT, LAY, Def::W, Def::U, false, ObsPixels>;
             const int cap = resident_blocks(reinterpret_cast<const void*>(kpix));
             if (nb > cap) nb = cap;
-            if (dev_cam) {  // (r06) the pre-queued LM evaluation: AoS, NT loads (ne_dev_ok)
+            if (db) {  // (r06) the pre-queued LM evaluation: AoS, NT loads (ne_dev_ok)
                 hipLaunchKernelGGL((k_normal_eq_dev<TagT, ACM_LAYOUT_AOS, Def::W, Def::U, true,
                                                     ObsCells>),
-                                   dim3(nb), dim3(kBlock), 0, s, dev_cam, n, points_3d,
+                                   dim3(nb), dim3(kBlock), 0, s, *db, n, points_3d,
                                    obs_cells(cells, *grid), invalid_policy, parts);
                 return;
             }
@@ -4670,9 +4670,9 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
             }
             const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
             if (nb > cap) nb = cap;
-            if (dev_cam) {  // (ne_dev_ok: the default W, U; AoS; NT loads)
+            if (db) {  // (ne_dev_ok: the default W, U; AoS; NT loads)
                 hipLaunchKernelGGL((k_normal_eq_dev<TagT, ACM_LAYOUT_AOS, Def::W, Def::U, true>),
-                                   dim3(nb), dim3(kBlock), 0, s, dev_cam, n, points_3d,
+                                   dim3(nb), dim3(kBlock), 0, s, *db, n, points_3d,
                                    ObsPixels{points_2d_obs}, invalid_policy, parts);
                 return;
             }
@@ -4680,7 +4680,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
                                ObsPixels{points_2d_obs}, invalid_policy, parts);
         };
         auto by_waves = [&](auto lay_c) {
-            if (dev_cam) {  // the default kernel's partition (nb), then the dev form
+            if (db) {  // the default kernel's partition (nb), then the doorbell form
                 if constexpr (Def::W == 1) go(lay_c, std::integral_constant<int, 1>{});
                 else if constexpr (Def::W == 4) go(lay_c, std::integral_constant<int, 4>{});
                 else go(lay_c, std::integral_constant<int, 3>{});

@@ -598,51 +598,49 @@ struct RadTan {
         const T S = c.uk[1];
         if (S > T(0)) {
             asm volatile("" : "+v"(k3));
-            // (r06) every decision exits the loop by a break rather than a
-            // state value tested at the top: no per-step state moves and
-            // selects, the same decisions
-            bool ok = false;
 #pragma unroll 1
-            for (int i = 0; i < 12; ++i) {
+            for (int i = 0; i < 12 && state == 0; ++i) {
                 const T x2 = x * x, y2 = y * y, xy = x * y;
                 const T s = x2 + y2;
-                if (!(s <= S)) break;  // outside the disk, or NaN
-                // (r05) the target folded into the FMA chains, s + 2 x^2
-                // from x^2, and J's sums chained as FMAs: 6 fewer VALU
-                // instructions per step than the r04 form, the same
-                // quantities to within a few ulps of their terms (far
-                // inside the certification bands)
-                const T rad = fma(fma(fma(k3, s, k2), s, k1), s, T(1));
-                const T ex = fma(x, rad, fma(p1d, xy, fma(p2, fma(T(2), x2, s), -tx)));
-                const T ey = fma(y, rad, fma(p1, fma(T(2), y2, s), fma(p2d, xy, -ty)));
-                const T en2 = fma(ex, ex, ey * ey);
-                if (en2 < lo) {  // :459 breaks before the step
-                    ok = true;
-                    break;
+                int st;
+                if (!(s <= S)) {
+                    st = 2;  // outside the disk, or NaN
+                } else {
+                    // (r05) the target folded into the FMA chains, s + 2 x^2
+                    // from x^2, and J's sums chained as FMAs: 6 fewer VALU
+                    // instructions per step than the r04 form, the same
+                    // quantities to within a few ulps of their terms (far
+                    // inside the certification bands)
+                    const T rad = fma(fma(fma(k3, s, k2), s, k1), s, T(1));
+                    const T ex = fma(x, rad, fma(p1d, xy, fma(p2, fma(T(2), x2, s), -tx)));
+                    const T ey = fma(y, rad, fma(p1, fma(T(2), y2, s), fma(p2d, xy, -ty)));
+                    const T en2 = fma(ex, ex, ey * ey);
+                    if (en2 < lo) {
+                        st = 1;  // :459 breaks before the step
+                    } else if (!(en2 > hi)) {
+                        st = 2;  // in the band, or NaN
+                    } else {
+                        const T cm = fma(fma(k3t, s, k2d), s, k1);
+                        const T w = cm + cm;
+                        const T j00 = fma(x2, w, fma(p1d, y, fma(p2s, x, rad)));
+                        const T j11 = fma(y2, w, fma(p1s, y, fma(p2d, x, rad)));
+                        const T j01 = fma(xy, w, fma(p1d, x, p2d * y));
+                        const T det = fma(j00, j11, -(j01 * j01));
+                        const T r0 = __builtin_amdgcn_rcp(det);
+                        const T id = fma(r0, fma(-det, r0, T(1)), r0);
+                        const T dx = fma(j11, ex, -(j01 * ey)) * id;
+                        const T dy = fma(j00, ey, -(j01 * ex)) * id;
+                        x -= dx;
+                        y -= dy;
+                        const T dn2 = fma(dx, dx, dy * dy);
+                        st = dn2 < lo ? 1 : (dn2 > hi ? 0 : 2);  // :503
+                    }
                 }
-                if (!(en2 > hi)) break;  // in the band, or NaN
-                const T cm = fma(fma(k3t, s, k2d), s, k1);
-                const T w = cm + cm;
-                const T j00 = fma(x2, w, fma(p1d, y, fma(p2s, x, rad)));
-                const T j11 = fma(y2, w, fma(p1s, y, fma(p2d, x, rad)));
-                const T j01 = fma(xy, w, fma(p1d, x, p2d * y));
-                const T det = fma(j00, j11, -(j01 * j01));
-                const T r0 = __builtin_amdgcn_rcp(det);
-                const T id = fma(r0, fma(-det, r0, T(1)), r0);
-                const T dx = fma(j11, ex, -(j01 * ey)) * id;
-                const T dy = fma(j00, ey, -(j01 * ex)) * id;
-                x -= dx;
-                y -= dy;
-                const T dn2 = fma(dx, dx, dy * dy);
-                if (dn2 < lo) {  // :503
-                    ok = true;
-                    break;
-                }
-                if (!(dn2 > hi)) break;
+                state = st;
             }
             px = x;
             py = y;
-            return ok;
+            return state == 1;
         }
 #pragma unroll 1
         for (int i = 0; i < 12 && state == 0; ++i) {

@@ -21,6 +21,7 @@
 
 #include "acm.h"
 #include "lm_core.hpp"
+#include "lm_doorbell.hpp"
 
 namespace acm {
 int set_error(int code, const std::string& msg);  // acm.hip (one last-error slot)
@@ -30,7 +31,7 @@ int normal_equations_impl(const acm_camera* cam, size_t n, const double* points_
                           void* workspace, size_t workspace_bytes, void* stream,
                           unsigned long long* flag, unsigned long long seq,
                           unsigned int* ticket, const uint32_t* cells,
-                          const acm_cell_grid* grid, const acm_camera* dev_cam);
+                          const acm_cell_grid* grid, const LmDoorbell* db);
 bool ne_dev_ok(int layout);
 int check_cell_grid(const acm_cell_grid* grid);
 int linear_system_qr_error(const acm_camera* cam, size_t n, const double* points_3d, int layout,
@@ -460,59 +461,6 @@ __global__ void k_lm_copy_publish(const double* __restrict__ src, double* __rest
     }
 }
 
-// (r06) The doorbell of the pre-queued LM evaluation (ACM_TUNE_LM_HOST_RESULT
-// 3).  The host queues [k_lm_doorbell | normal equations from the device
-// camera | epilogue] for evaluation k + 1 while evaluation k runs; when k's
-// results are in and the LM wants another point, the host writes the camera
-// into the mailbox and then the sequence number, and the evaluation is
-// already on the GPU: no launch between the host's decision and the kernel.
-// Mailbox: pinned, coherent host memory.
-struct LmMailbox {
-    unsigned long long seq;  // host: written last (release)
-    unsigned long long ack;  // k_lm_doorbell: seq when served, else seq | kLmNotServed
-    acm_camera cam;          // host: the parameters to evaluate
-};
-constexpr unsigned long long kLmCancel = 1ull << 62;     // host: no evaluation after all
-constexpr unsigned long long kLmNotServed = 1ull << 63;  // device: cancelled or timed out
-
-// One wave: every lane polls the sequence word (one request), with a bounded
-// wait (timeout_ticks of the constant-rate wall clock) so the grid always
-// drains; then copies the camera (22 dwords) to device memory with vector
-// stores, or marks it cancelled (model = -1) for the evaluation queued behind.
-__global__ __launch_bounds__(64) void k_lm_doorbell(const LmMailbox* mb, unsigned long long seq,
-                                                    acm_camera* __restrict__ dst,
-                                                    unsigned long long* ack,
-                                                    unsigned long long timeout_ticks) {
-    const unsigned long long t0 = wall_clock64();
-    bool served = false;
-    for (;;) {
-        const unsigned long long v =
-            __hip_atomic_load(&mb->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-        const unsigned long long u = ((unsigned long long)hi << 32) | lo;
-        if (u == seq) {
-            served = true;
-            break;
-        }
-        if (u == (seq | kLmCancel) || wall_clock64() - t0 > timeout_ticks) break;
-        __builtin_amdgcn_s_sleep(8);
-    }
-    constexpr int kWords = (int)(sizeof(acm_camera) / 4);
-    const unsigned lane = threadIdx.x;
-    if (served) {
-        if (lane < kWords)
-            reinterpret_cast<unsigned*>(dst)[lane] =
-                __hip_atomic_load(reinterpret_cast<const unsigned*>(&mb->cam) + lane,
-                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else if (lane == 0) {
-        dst->model = -1;
-    }
-    if (lane == 0)
-        __hip_atomic_store(ack, served ? seq : (seq | kLmNotServed), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 ACM_API void acm_lm_default_config(acm_lm_config* cfg) {
     if (!cfg) return;
     std::memset(cfg, 0, sizeof(*cfg));
@@ -555,7 +503,7 @@ static void lm_summarize(const acm::lm::State& st, acm_camera* cam, int P,
 }
 
 // (r06) The LM host loop with pre-queued evaluations (ACM_TUNE_LM_HOST_RESULT
-// 3; k_lm_doorbell above).  The same evaluations in the same order as the
+// 3; lm_doorbell.hpp).  The same evaluations in the same order as the
 // launch-per-evaluation loop, from the same kernel body: the same iterates.
 static int lm_doorbell_loop(acm_camera* cam, size_t n, const double* points_3d, int layout,
                             const double* points_2d, const uint32_t* cells,
@@ -563,6 +511,8 @@ static int lm_doorbell_loop(acm_camera* cam, size_t n, const double* points_3d, 
                             acm::lm::State& st, int P, double* pinned, unsigned long long& seq,
                             double* d_res, void* workspace, size_t ne_ws,
                             acm_lm_summary* summary, hipStream_t s) {
+    using acm::kLmCancel;
+    using acm::LmMailbox;
     struct Mailbox {
         LmMailbox* p = nullptr;
         ~Mailbox() {
@@ -585,24 +535,28 @@ static int lm_doorbell_loop(acm_camera* cam, size_t n, const double* points_3d, 
     if (hip_ok(hipGetDevice(&dev)) ||
         hip_ok(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev)) || khz <= 0)
         return sfail(ACM_ERR_HIP, "LM: wall clock rate unavailable");
-    // a doorbell not rung within 10 s ends its wait (the evaluation is then
-    // reported as failed): the queued kernels always drain
-    const unsigned long long timeout = 10000ull * (unsigned long long)khz;
     const int R = P * P + P + 2;
     auto* flag = reinterpret_cast<unsigned long long*>(pinned + 127);
     auto* ticket = reinterpret_cast<unsigned int*>(d_res + R);
-    auto* dev_cam = reinterpret_cast<acm_camera*>(d_res + R + 8);
-    auto* ack = &mb->ack;
-    if (hip_ok(hipMemsetAsync(ticket, 0, sizeof(unsigned int), s)))
+    // the spare words after the results: [ticket | device flag | ... |
+    // camera at +8]
+    acm::LmDoorbell db;
+    db.mb = mb;
+    db.flag = reinterpret_cast<unsigned long long*>(d_res + R + 1);
+    db.cam = reinterpret_cast<acm_camera*>(d_res + R + 8);
+    // a doorbell not rung within 10 s ends its wait (the evaluation is then
+    // reported as failed): the queued kernels always drain
+    db.timeout = 10000ull * (unsigned long long)khz;
+    if (hip_ok(hipMemsetAsync(d_res + R, 0, 2 * sizeof(double), s)))
         return sfail(ACM_ERR_HIP, "LM: ticket reset failed");
-    // queue evaluation `q`: the doorbell wait, then the normal equations and
+    auto* ack = &mb->ack;
+    // queue evaluation `q`: the normal equations behind the doorbell, then
     // their epilogue (results into the pinned buffer, completion word = q)
     auto enqueue = [&](unsigned long long q) -> int {
-        hipLaunchKernelGGL(k_lm_doorbell, dim3(1), dim3(64), 0, s, mb, q, dev_cam, ack, timeout);
-        if (hip_ok(hipGetLastError())) return sfail(ACM_ERR_HIP, "LM: doorbell launch");
+        db.seq = q;
         return acm::normal_equations_impl(cam, n, points_3d, layout, points_2d,
                                           cfg->invalid_policy, pinned, workspace, ne_ws, s, flag,
-                                          q, ticket, cells, grid, dev_cam);
+                                          q, ticket, cells, grid, &db);
     };
     auto ring = [&](unsigned long long q, const double* x) {
         acm_camera c = *cam;
@@ -610,8 +564,7 @@ static int lm_doorbell_loop(acm_camera* cam, size_t n, const double* points_3d, 
         std::memcpy(&mb->cam, &c, sizeof(c));
         __atomic_store_n(&mb->seq, q, __ATOMIC_RELEASE);
     };
-    // spin on evaluation q's completion word (as the mode-2 loop), then
-    // check that its doorbell served it
+    // spin on evaluation q's completion word (as the mode-2 loop)
     auto wait = [&](unsigned long long q) -> int {
         for (unsigned spin = 1;; ++spin) {
             if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == q) break;

@@ -661,7 +661,10 @@ ACM_API int acm_stream_synchronize(void *stream);
  * has the normal-equations kernel write its results straight into pinned
  * host memory rather than device memory plus a copy: 0 = off, 1 = on with a
  * stream synchronisation, 2 = on with the host spinning on a completion
- * word the kernel publishes; -1 = auto = 2.
+ * word the kernel publishes, 3 = as 2 with each evaluation queued ahead of
+ * the host's decision and released by a host-written doorbell (AoS points,
+ * default NE knobs; else 2); -1 = auto = 2.  Every mode takes the same
+ * iterates.
  * ACM_TUNE_SAMPLE_FUSED: acm_sample_points' kernels.  -1 = auto (r03) = the
  * speculative segment path (4, below) for RadTan, else the segment two-pass path (certified per-segment counts, offsets by a scan,
  * then a write pass with known offsets); 0 = the round-1 two-pass count /

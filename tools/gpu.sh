@@ -17,8 +17,8 @@
 #                      KERNELS) + profiles/summarize_kernels.py
 #   rows               tools/bench_rows.py (every SURVEY 8(a) row vs oracle)
 #   configs[=LIST]     tools/bench_configs.py --configs LIST (default 1,3,4,5)
-#   sample             rocprofv3 kernel trace of tools/diag_sample.py
-#   radtan_tail        tools/diag_radtan_tail.py (config-4 pixels)
+#   sample             rocprofv3 kernel trace of tools/probes.py sample
+#   radtan_tail        tools/probes.py radtan_tail (config-4 pixels)
 #   e2e                tools/bench_e2e.py (PCIe-inclusive rate)
 #   run:NAME:CMD       any command (words split on '+'), output to <TAG>_NAME.log
 #   kt:NAME:CMD        rocprofv3 kernel trace of a python3 CMD
@@ -93,10 +93,10 @@ for step in "$@"; do
     check $? configs; grep -h '"config"' $O/${TAG}_configs.log | cut -c1-220 ;;
   sample)
     VARIANTS=seg timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d $O/${TAG}_sprof -o kt -- python3 tools/diag_sample.py > $O/${TAG}_sample.log 2>&1
+      -d $O/${TAG}_sprof -o kt -- python3 tools/probes.py sample > $O/${TAG}_sample.log 2>&1
     check $? sample ;;
   radtan_tail)
-    timeout -k 10 300 python tools/diag_radtan_tail.py > $O/${TAG}_radtan_tail.log 2>&1
+    timeout -k 10 300 python tools/probes.py radtan_tail > $O/${TAG}_radtan_tail.log 2>&1
     check $? radtan_tail ;;
   e2e)
     timeout -k 10 300 python tools/bench_e2e.py > $O/${TAG}_e2e.log 2>&1
