@@ -23,7 +23,9 @@ ALL = ("radtan_unproject", "kb_unproject", "kb_normal_eq", "fov_grid", "sample_k
 # equations on the config-3 (9.29M) / config-5 (92.9M) KB-sampled
 # correspondences at the DS linear estimate (the LM's inner loop);
 # "ds_reproj9" / "ds_reproj93", compute_reprojection_error on the same data;
-# "ds_prologue9" / "ds_prologue93", the initial error + linear estimation
+# "ds_prologue9" / "ds_prologue93", the initial error + linear estimation;
+# "ds_ne93c" / "ds_reproj93c" / "ds_prologue93c" (r06): the same three at
+# 92.9M on the cell form config 5 now runs (4-B cells instead of 16-B pixels)
 
 
 def main():
@@ -149,6 +151,30 @@ def main():
             ms = timed(lambda: util.compute_reprojection_error(ds, sxyz, suv))
             emit(rtag, sxyz.shape[0], ms, 48)
         del suv, sxyz
+    if want & {"ds_ne93c", "ds_reproj93c", "ds_prologue93c"}:
+        suv, sxyz, cs = util.sample_points(src, 100_000_000, cells=True)
+        n = sxyz.shape[0]
+        if "ds_prologue93c" in want:  # reads 28 B, writes 8 B per point
+            ms = timed(lambda: util.initial_error_and_linear_estimation(
+                conversion._init_target("double_sphere", src), sxyz, suv, cells=cs))
+            emit("ds_prologue93c", n, ms, 36)
+        ds = conversion._init_target("double_sphere", src)
+        ds.linear_estimation(sxyz, suv)
+        if "ds_ne93c" in want:  # reads 28 B per point
+            cam = ds.acm_camera()
+            wsb = L.acm_normal_equations_workspace_size(3, n)
+            ws = torch.empty((wsb // 8 + 1,), dtype=torch.float64, device="cuda")
+            out = torch.empty((6 * 6 + 6 + 2,), dtype=torch.float64, device="cuda")
+            sh = torch.cuda.current_stream().cuda_stream
+            ms = timed(lambda: L.acm_normal_equations_cells(
+                ctypes.byref(cam), n, sxyz.data_ptr(), 0, cs.cells.data_ptr(),
+                ctypes.byref(cs.grid), 0, out.data_ptr(), ws.data_ptr(), wsb, sh))
+            emit("ds_ne93c", n, ms, 28)
+            del ws
+        if "ds_reproj93c" in want:  # reads 28 B, writes 8 B per point
+            ms = timed(lambda: util.compute_reprojection_error(ds, sxyz, suv, cells=cs))
+            emit("ds_reproj93c", n, ms, 36)
+        del suv, sxyz, cs
     if "sample_kb" in want:
         if a.sample_fused is not None:
             L.acm_set_tuning(_lib.TUNE_SAMPLE_FUSED, a.sample_fused)
