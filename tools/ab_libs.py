@@ -103,7 +103,18 @@ def main():
             outs.append((tag, [t.clone() for t in (uv, st, rays, st2)]))
         same = all(torch.equal(x.view(torch.uint8), y.view(torch.uint8))
                    for _, o in outs[1:] for x, y in zip(outs[0][1], o))
-        print(json.dumps({"call": f"round_trip_{nm}", "same_bits": same}), flush=True)
+        rec = {"call": f"round_trip_{nm}", "same_bits": same}
+        if not same:  # which outputs differ, and the rays by how much
+            o0, o1 = outs[0][1], outs[-1][1]
+            rec["same_pixels_and_statuses"] = (
+                torch.equal(o0[0].view(torch.uint8), o1[0].view(torch.uint8))
+                and torch.equal(o0[1], o1[1]) and torch.equal(o0[3], o1[3]))
+            f0, f1 = torch.isfinite(o0[2]), torch.isfinite(o1[2])
+            rec["same_ray_finiteness"] = torch.equal(f0, f1)
+            both = f0 & f1
+            rec["max_ray_abs_diff"] = float((o0[2][both] - o1[2][both]).abs().max())
+            rec["rays_differing"] = int(((o0[2] != o1[2]) & both).any(1).sum())
+        print(json.dumps(rec), flush=True)
         del outs
     del pts, uv, st, rays, st2
     n = a.points

@@ -97,18 +97,21 @@ def lm_wall(src, xyz, uv, target, reps=5):
             "termination": res.termination}
 
 
-def warm_convert(src, xyz, uv, reps=3):
+def warm_convert(src, xyz, uv, reps=3, cells=None):
     """conversion.convert to double_sphere (camera_converter.rs:355-488),
     wall: one untimed call first (the caching allocator's first multi-GB
-    workspaces and the first launches), then the fastest of `reps`."""
+    workspaces and the first launches), then the fastest of `reps`.
+    cells (r06): the util.CellSample of uv -- the cell form bench.py's
+    config-5 leg runs (same results)."""
     import torch
     from apex_camera_models import conversion
-    conversion.convert(src, "double_sphere", xyz, uv)
+    kw = {"cells": cells} if cells is not None else {}
+    conversion.convert(src, "double_sphere", xyz, uv, **kw)
     best, met = float("inf"), None
     for _ in range(reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        met = conversion.convert(src, "double_sphere", xyz, uv)
+        met = conversion.convert(src, "double_sphere", xyz, uv, **kw)
         best = min(best, time.perf_counter() - t0)
     return met, best
 
@@ -331,6 +334,16 @@ def config5(n_cells):
           "termination": met.lm_termination,
           "final_mean_px": met.final_reprojection_error.mean,
           "final_rmse_px": met.final_reprojection_error.rmse})
+    del uv, xyz
+    torch.cuda.empty_cache()
+    uv, xyz, cs = util.sample_points(src, n_cells, cells=True)
+    met_c, t_cc = warm_convert(src, xyz, uv, cells=cs)
+    emit({"config": 5, "what": "KB->DS conversion on the cell form (convert(cells=...), as "
+                               "bench.py's config5; wall, warm, best of 3)",
+          "correspondences": int(xyz.shape[0]), "convert_s": round(t_cc, 4),
+          "lm_iterations": met_c.lm_iterations,
+          "same_params_as_pixels": met_c.model.params() == met.model.params()})
+    del cs
     ds = met.model
     uv64, st64, _ = ds.project_batch(xyz)
     uv32, st32, _ = ds.project_batch(xyz.to(torch.float32))
