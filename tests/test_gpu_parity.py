@@ -131,7 +131,7 @@ def test_newton_reference_loop_bit_exact(be, golden_dir, model):
 
 
 # strongly distorted cameras inside the fast loops' per-camera bounds (and one
-# RadTan camera outside them), as in tools/diag_newton_fast.py
+# RadTan camera outside them), as in round 2's newton_fast probe (git history)
 NEWTON_STRESS = [
     (2, [190.97847715128717, 190.9733070521226, 254.93170605935475, 256.8974428996504,
          0.5, -0.3, 0.1, -0.02], (512, 512)),
