@@ -87,6 +87,16 @@ def main():
         out[f"lm_err_{tgt}"] = np.array([fe.mean, fe.median, fe.n_valid])
         ie = met.initial_reprojection_error
         out[f"init_err_{tgt}"] = np.array([ie.mean, ie.median, ie.n_valid, ie.min, ie.max])
+    # --- (r06) the same conversion on the cell form: each rank's slice of
+    # the cells, the sharded opening / LM / final error reading 4-B cells
+    uv_c, xyz_c, cs = util.sample_points(src, 4000, cells=True)
+    shard_cs = util.CellSample(cells=cs.cells[slo:shi], grid=cs.grid)
+    met = conversion.convert(src, "double_sphere", xyz_c[slo:shi], uv_c[slo:shi],
+                             collective=coll, cells=shard_cs)
+    out["cells_params"] = np.array(met.model.params())
+    fe, ie = met.final_reprojection_error, met.initial_reprojection_error
+    out["cells_err"] = np.array([met.lm_iterations, fe.mean, fe.median, fe.n_valid, ie.mean,
+                                 ie.median, ie.n_valid])
     np.savez(os.path.join(a.out, f"rank{rank}.npz"), **out)
     dist.barrier()
     dist.destroy_process_group()

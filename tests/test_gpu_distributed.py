@@ -106,4 +106,19 @@ def test_sharded_gpu_path_matches_single_process(world, tmp_path):
         tol = 1e-4 if tgt == "rad_tan" else 1e-5
         assert abs(fe[0] - ref.final_reprojection_error.mean) <= \
             tol * ref.final_reprojection_error.mean + 1e-12
+
+    # (r06) the sharded conversion on the cell form: every rank the same
+    # bits, the pixel-form sharded run's parameters (the same sums: the cell
+    # kernels rebuild the pixels exactly), and the 1-GPU run's to rounding
+    ref = conversion.convert(src, "double_sphere", xyz_all, uv_all)
+    for r in res:
+        assert np.array_equal(r["cells_params"], res[0]["cells_params"])
+        assert np.array_equal(r["cells_err"], res[0]["cells_err"])
+        assert np.array_equal(r["cells_params"], r["lm_params_double_sphere"])
+    np.testing.assert_allclose(res[0]["cells_params"], ref.model.params(), rtol=1e-8,
+                               atol=1e-10)
+    ce = res[0]["cells_err"]
+    assert ce[3] == ref.final_reprojection_error.n_valid
+    assert ce[6] == ref.initial_reprojection_error.n_valid
+    assert ce[5] == ref.initial_reprojection_error.median
     torch.cuda.synchronize()
