@@ -1524,7 +1524,7 @@ __device__ __forceinline__ double reproj_error(const Cam<double>& c, double x, d
     const uint8_t st = M::template project<false>(c, x, y, z, u, v, nullptr, nullptr);
     if (st != ST_OK) return __builtin_nan("");
     const double du = u - o.x, dv = v - o.y;
-    return sqrt(du * du + dv * dv);
+    return sqrt_rn(du * du + dv * dv);
 }
 
 // the median's pass-0 digit of an error (bits 53..63, k_sel_hist's pass 0)
@@ -2823,7 +2823,7 @@ __device__ __forceinline__ void tri_add_row(double (&R)[Tri<M>::S], double (&row
         const double b = row[j];
         if (b != 0.0) {
             const double a = R[Tri<M>::at(j, j)];
-            const double r = sqrt(a * a + b * b);
+            const double r = sqrt_rn(a * a + b * b);
             const double c = a / r, s = b / r;
             R[Tri<M>::at(j, j)] = r;
 #pragma unroll
@@ -2852,7 +2852,7 @@ __device__ __forceinline__ void tri_add_rows(double (&R)[Tri<M>::S], double (&ro
         for (int i = 0; i < NR; ++i) sig += rows[i][j] * rows[i][j];
         if (sig != 0.0) {
             const double x0 = R[Tri<M>::at(j, j)];
-            const double nrm = sqrt(x0 * x0 + sig);
+            const double nrm = sqrt_rn(x0 * x0 + sig);
             const double v0 = x0 >= 0.0 ? x0 + nrm : x0 - nrm;  // no cancellation
             const double beta = 2.0 / (v0 * v0 + sig);
             // new diagonal -sign(x0) nrm, flipped to +nrm with its row
@@ -2895,7 +2895,7 @@ struct LinRows<ACM_KANNALA_BRANDT> {  // kannala_brandt.rs:184-259, k = 4
                                 double v, double (&r0)[K + 1], double (&r1)[K + 1], int& err) {
         const double fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
         if (Z <= kEps) return false;  // :195-197
-        const double r = sqrt(X * X + Y * Y);
+        const double r = sqrt_rn(X * X + Y * Y);
         const double theta = atan2(r, Z);
         const double t2 = theta * theta, t3 = t2 * theta, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
         r0[0] = r1[0] = t3; r0[1] = r1[1] = t5; r0[2] = r1[2] = t7; r0[3] = r1[3] = t9;
@@ -2914,7 +2914,7 @@ struct LinRowsAlpha {  // double_sphere.rs:242-258 (= ucm.rs, eucm.rs), k = 1
     __device__ static bool rows(const Cam<double>& c, double X, double Y, double Z, double u,
                                 double v, double (&r0)[K + 1], double (&r1)[K + 1], int&) {
         const double fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
-        const double d = sqrt(X * X + Y * Y + Z * Z);
+        const double d = sqrt_rn(X * X + Y * Y + Z * Z);
         const double u_cx = u - cx, v_cy = v - cy;
         r0[0] = u_cx * (d - Z);
         r1[0] = v_cy * (d - Z);
@@ -3181,7 +3181,7 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid(acm_camera cam, size_t n
             double x, y, z;
             load_point<LAYOUT>(pts, n, i, x, y, z);
             const double r2 = x * x + y * y;  // :192-193
-            const double r = sqrt(r2);
+            const double r = sqrt_rn(r2);
             const double u0 = obs[2 * i], v0 = obs[2 * i + 1];
             sx[t] = x; sy[t] = y; sz[t] = z;
             su[t] = u0; sv[t] = v0;
@@ -3323,7 +3323,7 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid_rec(acm_camera cam, size
         } else {
             double x, y, z;
             load_point<LAYOUT>(pts, n, i, x, y, z);
-            const double r2 = x * x + y * y, rr = sqrt(r2);
+            const double r2 = x * x + y * y, rr = sqrt_rn(r2);
             const double rd = fov_rd_general(tw2, rr, z, w, r2, rd0);
             const double mx = x * rd, my = y * rd;
             du = (fx * mx + cx) - obs[2 * i];
@@ -3342,7 +3342,7 @@ __global__ __launch_bounds__(kFovBlock) void k_fov_grid_rec(acm_camera cam, size
             double x, y, z;
             load_point<LAYOUT>(pts, n, i, x, y, z);
             const double r2 = x * x + y * y;  // :192-193
-            const double r = sqrt(r2);
+            const double r = sqrt_rn(r2);
             const double u0 = obs[2 * i], v0 = obs[2 * i + 1];
             const bool fast = z > 0.0 && r > 0.0 && z < INFINITY && r < INFINITY;
             double2* o = reinterpret_cast<double2*>(&srec[t][0]);
@@ -3431,7 +3431,7 @@ __global__ __launch_bounds__(kFovPlBlock) void k_fov_grid_pl(acm_camera cam, siz
                 double x, y, z;
                 load_point<LAYOUT>(pts, n, i, x, y, z);
                 const double r2 = x * x + y * y;  // fov.rs:192-193
-                const double r = sqrt(r2);
+                const double r = sqrt_rn(r2);
                 const double u0 = obs[2 * i], v0 = obs[2 * i + 1];
                 const bool fast = z > 0.0 && r > 0.0 && z < INFINITY && r < INFINITY;
                 const bool small = r2 < kEpsSqrt;
@@ -3473,7 +3473,7 @@ __global__ __launch_bounds__(kFovPlBlock) void k_fov_grid_pl(acm_camera cam, siz
                     if (i < n && fl[j] == 0.0 && ir[j] == 0.0) {
                         double x, y, z;
                         load_point<LAYOUT>(pts, n, i, x, y, z);
-                        const double r2 = x * x + y * y, rr = sqrt(r2);
+                        const double r2 = x * x + y * y, rr = sqrt_rn(r2);
                         const double rdg = fov_rd_general(tw2, rr, z, w, r2, rd0);
                         const double du = (fx * (x * rdg) + cx) - obs[2 * i];
                         const double dv = (fy * (y * rdg) + cy) - obs[2 * i + 1];

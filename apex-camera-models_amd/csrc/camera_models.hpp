@@ -220,6 +220,37 @@ __device__ __forceinline__ bool nr_range(double a) {
     return a >= 0x1p-1000 && a <= 0x1p1000;
 }
 
+// (r06) sqrt(a) correctly rounded, bit for bit the compiler's f64 sqrt: its
+// expansion is v_rsq_f64 and the two Goldschmidt / Newton corrections below,
+// wrapped in a rescaling of inputs under 2^-767 and a fixup for 0 and inf
+// (10 of its ~20 VALU instructions).  Here the same ten-instruction core runs
+// for a in [2^-767, DBL_MAX] and the full sqrt() for the rest (0, the
+// rescaled range, inf, NaN, negative), laid out as a cold branch that a wave
+// skips when none of its lanes needs it (computed unconditionally and
+// selected, as the compiler does without the expectation, both paths cost
+// more than the one sqrt).  Same operations in the same order on the range
+// where the compiler's version does not rescale, so the same bits.
+template <class T>
+__device__ __forceinline__ T sqrt_rn(T a) {
+    if constexpr (sizeof(T) == 8) {
+        if (__builtin_expect(a >= 0x1p-767 && a <= 0x1.fffffffffffffp1023, 1)) {
+            const double y = __builtin_amdgcn_rsq(a);
+            double g = a * y;
+            double h = y * 0.5;
+            const double r = fma(-h, g, 0.5);
+            g = fma(g, r, g);
+            h = fma(h, r, h);
+            double d = fma(-g, g, a);
+            g = fma(d, h, g);
+            d = fma(-g, g, a);
+            return fma(d, h, g);
+        }
+        return sqrt(a);
+    } else {
+        return sqrt(a);
+    }
+}
+
 // sin and cos of theta in [0, 2] (KB's unprojection angle, at most ~pi/2):
 // theta * S(theta^2) and C(theta^2), S and C the degree-10 Chebyshev
 // interpolants of sin(sqrt(s))/sqrt(s) and cos(sqrt(s)) on s in [0, 4]
@@ -440,7 +471,7 @@ struct Pinhole {
         T mx = div_by_f(u - cx, fx, c.ifx);  // (u - cx) / fx
         T my = div_by_f(v - cy, fy, c.ify);
         T r2 = mx * mx + my * my;
-        T norm = sqrt(T(1) + r2);
+        T norm = sqrt_rn(T(1) + r2);
         T ninv = T(1) / norm;
         X = mx * ninv;
         Y = my * ninv;
@@ -686,7 +717,7 @@ struct RadTan {
     }
     // :520-524: (x, y, 1).normalize()
     __device__ static __forceinline__ uint8_t newton_finish(const Newton& s, T& X, T& Y, T& Z) {
-        T n = sqrt(s.px * s.px + s.py * s.py + T(1) * T(1));
+        T n = sqrt_rn(s.px * s.px + s.py * s.py + T(1) * T(1));
         const T nq[2] = {s.px, s.py};
         T q[2];
         Z = div_shared(nq, n, q);  // X = px / n, Y = py / n, Z = 1 / n
@@ -760,7 +791,7 @@ struct KannalaBrandt {
                 const T at = atan01(q);
                 theta = swap ? T(1.5707963267948966) - at : at;
             } else {
-                r = sqrt(r2);
+                r = sqrt_rn(r2);
                 theta = atan2_ge0(r, z);  // :365 (r >= 0)
                 ir = T(1) / r;
             }
@@ -768,7 +799,7 @@ struct KannalaBrandt {
         } else
 #endif
         {
-            r = sqrt(r2);
+            r = sqrt_rn(r2);
             theta = EXACT ? atan2_exact(r, z) : atan2_ge0(r, z);  // :365 (r >= 0)
             axis = r < T(kEps);  // :375
             if (FAST) ir = T(1) / r;
@@ -824,13 +855,13 @@ struct KannalaBrandt {
             const T at = atan01(q);
             theta = swap ? T(1.5707963267948966) - at : at;
         } else {
-            r = sqrt(r2);
+            r = sqrt_rn(r2);
             theta = atan2_ge0(r, z);
             ir = T(1) / r;
         }
         axis = r2 < T(kAxisR2);
 #else
-        r = sqrt(r2);
+        r = sqrt_rn(r2);
         theta = atan2_ge0(r, z);
         axis = r < T(kEps);
         ir = T(1) / r;
@@ -1074,7 +1105,7 @@ struct KannalaBrandt {
         }
 #endif
         if (!certified) {  // the reference's sequence (:462-525)
-            ru = sqrt(r2);
+            ru = sqrt_rn(r2);
             ru = fmin(ru, T(kPi / 2.0));  // :467, f64::min semantics
             theta = ru;
             if (ru > PREC) {
@@ -1131,7 +1162,7 @@ struct KannalaBrandt {
             const T yc = small ? T(0) : my * ir;
             const T px = s * xc, py = s * yc;
             const T n2 = px * px + py * py + co * co;
-            const T in = nr_range(n2) ? rsq_nr(n2) : T(1) / sqrt(n2);
+            const T in = nr_range(n2) ? rsq_nr(n2) : T(1) / sqrt_rn(n2);
             X = px * in;
             Y = py * in;
             Z = co * in;
@@ -1147,7 +1178,7 @@ struct KannalaBrandt {
         T yc = small ? T(0) : c2[1];
         T px = s * xc, py = s * yc;
         T n2 = px * px + py * py + co * co;
-        T n = sqrt(n2);
+        T n = sqrt_rn(n2);
         const T nq[3] = {px, py, co};
         T q[3];
         div_shared(nq, n, q);
@@ -1170,9 +1201,9 @@ struct DoubleSphere {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
         const T alpha = c.p[4], xi = c.p[5];
         T r_squared = (x * x) + (y * y);
-        T d1 = sqrt(r_squared + (z * z));
+        T d1 = sqrt_rn(r_squared + (z * z));
         T gamma = xi * d1 + z;
-        T d2 = sqrt(r_squared + gamma * gamma);
+        T d2 = sqrt_rn(r_squared + gamma * gamma);
         T denom = alpha * d2 + (T(1) - alpha) * gamma;
         // w2 (from w1): a camera constant, computed once per camera with the
         // same IEEE operations (acm.hip unproject_consts, uk[1]; r05: it cost
@@ -1214,13 +1245,13 @@ struct DoubleSphere {
         const bool cond = !(alpha > T(0.5) && r_squared > c.uk[0]);
         const bool reject = alpha != T(0) && !cond;
         T mz = (T(1) - alpha * alpha * r_squared) /
-               (alpha * sqrt(T(1) - (T(2) * alpha - T(1)) * r_squared) + gamma_ds);
+               (alpha * sqrt_rn(T(1) - (T(2) * alpha - T(1)) * r_squared) + gamma_ds);
         T mz_squared = mz * mz;
-        T num = mz * xi + sqrt(mz_squared + (T(1) - xi * xi) * r_squared);
+        T num = mz * xi + sqrt_rn(mz_squared + (T(1) - xi * xi) * r_squared);
         T denom = mz_squared + r_squared;
         T coeff = num / denom;
         T px = coeff * mx, py = coeff * my, pz = coeff * mz - xi;
-        T n = sqrt(px * px + py * py + pz * pz);
+        T n = sqrt_rn(px * px + py * py + pz * pz);
         const T nq[3] = {px, py, pz};
         T q[3];
         div_shared(nq, n, q);
@@ -1240,7 +1271,7 @@ struct Ucm {
     __device__ static __forceinline__ uint8_t project(const Cam<T>& c, T x, T y, T z, T& u,
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], alpha = c.p[4];
-        T d = sqrt(x * x + y * y + z * z);
+        T d = sqrt_rn(x * x + y * y + z * z);
         T denom = alpha * d + (T(1) - alpha) * z;
         const T w = c.uk[2];  // per camera (acm.hip unproject_consts, r05)
         const bool ok = !(denom < T(1e-3)) && (z > -w * d);
@@ -1272,13 +1303,13 @@ struct Ucm {
         T mx = div_by_f(u - cx, fx, c.ifx) * gamma;  // (u - cx) / fx * gamma
         T my = div_by_f(v - cy, fy, c.ify) * gamma;
         T r_squared = mx * mx + my * my;
-        T num = xi + sqrt(T(1) + (T(1) - xi * xi) * r_squared);
+        T num = xi + sqrt_rn(T(1) + (T(1) - xi * xi) * r_squared);
         T denom = T(1) - r_squared;
         // c.uk[1] = gamma * gamma / (2 alpha - 1)
         const bool cond = alpha > T(0.5) ? (r_squared <= c.uk[1]) : true;
         T coeff = num / denom;
         T px = coeff * mx, py = coeff * my, pz = coeff - xi;
-        T n = sqrt(px * px + py * py + pz * pz);
+        T n = sqrt_rn(px * px + py * py + pz * pz);
         const T nq[3] = {px, py, pz};
         T q[3];
         div_shared(nq, n, q);
@@ -1300,7 +1331,7 @@ struct Eucm {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3];
         const T alpha = c.p[4], beta = c.p[5];
         T rr = x * x + y * y;
-        T d = sqrt(beta * rr + z * z);
+        T d = sqrt_rn(beta * rr + z * z);
         T denom = alpha * d + (T(1) - alpha) * z;
         bool cond = true;
         if (alpha > T(0.5)) {
@@ -1341,11 +1372,11 @@ struct Eucm {
         T gamma = T(1) - alpha;
         T num = T(1) - r_squared * alpha * alpha * beta;
         T det = T(1) - (alpha - gamma) * beta * r_squared;
-        T denom = gamma + alpha * sqrt(det);
+        T denom = gamma + alpha * sqrt_rn(det);
         // c.uk[0] = 1 / beta * (2 alpha - 1)
         const bool cond = !(alpha > T(0.5) && r_squared > c.uk[0]);
         T mz = num / denom;
-        T n = sqrt(mx * mx + my * my + mz * mz);
+        T n = sqrt_rn(mx * mx + my * my + mz * mz);
         const T nq[3] = {mx, my, mz};
         T q[3];
         div_shared(nq, n, q);
@@ -1366,7 +1397,7 @@ struct Fov {
                                                       T& v, T* ju, T* jv) {
         const T fx = c.p[0], fy = c.p[1], cx = c.p[2], cy = c.p[3], wf = c.p[4];
         T r2 = x * x + y * y;
-        T r = sqrt(r2);
+        T r = sqrt_rn(r2);
         const T tan_w_half = c.p[8];  // tan(w / 2), host-precomputed (acm.hip prep)
         T atan_wrd = EXACT ? atan2_exact(T(2) * tan_w_half * r, z)  // y >= 0
                            : atan2_ge0(T(2) * tan_w_half * r, z);
@@ -1420,7 +1451,7 @@ struct Fov {
                     py = (my * ru) * ic;
                 }
                 const T n2 = fma(px, px, fma(py, py, T(1)));
-                const T in = nr_range(n2) ? rsq_nr(n2) : T(1) / sqrt(n2);
+                const T in = nr_range(n2) ? rsq_nr(n2) : T(1) / sqrt_rn(n2);
                 X = px * in;
                 Y = py * in;
                 Z = in;
@@ -1428,7 +1459,7 @@ struct Fov {
             }
         }
 #endif
-        T rd = sqrt(mx * mx + my * my);
+        T rd = sqrt_rn(mx * mx + my * my);
         T px = mx, py = my;
         if (mul2 > T(kEpsSqrt) && rd > T(kEpsSqrt)) {
             T srw, crw;
@@ -1440,7 +1471,7 @@ struct Fov {
             px = q[0];
             py = q[1];
         }
-        T n = sqrt(px * px + py * py + T(1) * T(1));
+        T n = sqrt_rn(px * px + py * py + T(1) * T(1));
         const T nq[2] = {px, py};
         T q[2];
         Z = div_shared(nq, n, q);  // X = px / n, Y = py / n, Z = 1 / n

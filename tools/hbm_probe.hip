@@ -368,3 +368,34 @@ extern "C" int acm_probe_round_trip(size_t n, const double* xyz, double* uv, uin
                        st, rays, st2);
     return (int)hipGetLastError();
 }
+
+// (r06) camera_models.hpp's sqrt_rn against the compiler's sqrt, bit for bit
+// (tests/test_gpu_sqrt_rn.py): *mismatches counts the inputs whose results
+// differ; the first few (input, sqrt, sqrt_rn) triples go to `first`.
+#include "../apex-camera-models_amd/csrc/camera_models.hpp"
+
+__global__ __launch_bounds__(256) void k_sqrt_rn_check(const double* __restrict__ a, size_t n,
+                                                       unsigned long long* mismatches,
+                                                       double* first) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double x = a[i];
+    const double r0 = sqrt(x);
+    const double r1 = acm::sqrt_rn(x);
+    if (__double_as_longlong(r0) != __double_as_longlong(r1)) {
+        const unsigned long long k = atomicAdd(mismatches, 1ull);
+        if (k < 8) {
+            first[3 * k] = x;
+            first[3 * k + 1] = r0;
+            first[3 * k + 2] = r1;
+        }
+    }
+}
+
+extern "C" int acm_probe_sqrt_rn(const double* a, size_t n, unsigned long long* mismatches,
+                                 double* first, void* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_sqrt_rn_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, a, n, mismatches, first);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+}
