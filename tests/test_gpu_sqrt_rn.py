@@ -38,9 +38,10 @@ def test_sqrt_rn_is_the_compiler_sqrt():
         tested += a.numel()
 
     for k in range(3):
-        bits = torch.randint(0, 2 ** 62, (n,), device="cuda", generator=g, dtype=torch.int64)
-        check((bits & ~(1 << 63)).view(torch.float64))  # every exponent, sign bit clear
-        check(bits.view(torch.float64))                 # and negatives
+        bits = torch.randint(-2 ** 63, 2 ** 63 - 1, (n,), device="cuda", generator=g,
+                             dtype=torch.int64)
+        check((bits & 0x7FFFFFFFFFFFFFFF).view(torch.float64))  # every exponent, sign clear
+        check(bits.view(torch.float64))                         # and both signs
         x = torch.randn(n, device="cuda", generator=g, dtype=torch.float64) * 10.0 ** (3 * k - 3)
         y = torch.randn(n, device="cuda", generator=g, dtype=torch.float64) * 10.0 ** (3 * k - 3)
         check(x * x + y * y)
