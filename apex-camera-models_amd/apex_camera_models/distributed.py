@@ -128,21 +128,34 @@ class RcclCollective:
     def __init__(self, group=None):
         from . import _lib
         L = _lib.load()
-        if not L.acm_rccl_available():
-            raise RuntimeError("librccl.so.1 is not loadable: no RCCL collective")
+        self.c = None
         if dist.is_available() and dist.is_initialized():
             self.world = dist.get_world_size(group)
             self.rank = dist.get_rank(group)
         else:  # no process group: a 1-rank communicator (bench.py's world-1 leg)
             self.world, self.rank = 1, 0
+        ok = int(bool(L.acm_rccl_available()))
+        if self.world > 1:  # the same answer on every rank (see below)
+            dev = torch.device("cuda", torch.cuda.current_device()) \
+                if dist.get_backend(group) == "nccl" else torch.device("cpu")
+            t = torch.tensor([ok], dtype=torch.int32, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+            ok = int(t.item())
+        if not ok:
+            raise RuntimeError("librccl.so.1 is not loadable on every rank: no RCCL collective")
+        self.c = None
         uid = (ctypes.c_uint8 * _lib.RCCL_UNIQUE_ID_BYTES)()
-        if self.rank == 0:
-            _lib.check(L.acm_rccl_unique_id(uid))
-        obj = [bytes(uid)]
+        rc = L.acm_rccl_unique_id(uid) if self.rank == 0 else 0
+        obj = [rc, bytes(uid)]
         if self.world > 1:
+            # every rank learns whether rank 0 could make the id, so a failure
+            # raises on all ranks alike instead of leaving the others blocked
+            # in the communicator's rendezvous
             src = dist.get_global_rank(group, 0) if group is not None else 0
             dist.broadcast_object_list(obj, src=src, group=group)
-        uid = (ctypes.c_uint8 * _lib.RCCL_UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
+        if obj[0] != 0:
+            raise RuntimeError(f"acm_rccl_unique_id failed on rank 0 ({obj[0]})")
+        uid = (ctypes.c_uint8 * _lib.RCCL_UNIQUE_ID_BYTES).from_buffer_copy(obj[1])
         self.c = _lib.AcmCollective()
         _lib.check(L.acm_rccl_init(uid, self.world, self.rank, ctypes.byref(self.c)))
 
@@ -175,9 +188,15 @@ class LocalCollective:
 
 def make_collective(group=None):
     """The sharded conversion's collective for `group`: RcclCollective under
-    the nccl (RCCL) backend with one GPU per rank, else TorchCollective."""
+    the nccl (RCCL) backend with one GPU per rank, else TorchCollective --
+    also when RCCL cannot be set up; RcclCollective raises on every rank
+    alike before the communicator's rendezvous, so the fallback is taken by
+    all ranks together (the bench line names the collective it used)."""
     if dist.get_backend(group) == "nccl":
-        return RcclCollective(group)
+        try:
+            return RcclCollective(group)
+        except RuntimeError:
+            pass
     return TorchCollective(group)
 
 
