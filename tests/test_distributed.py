@@ -119,3 +119,23 @@ def test_sharded_exchange_matches_single_process(world, tmp_path):
     offs = [int(r["sp_off"][0]) for r in res]
     assert offs == list(np.cumsum([0] + [len(r["sp_uv"]) for r in res[:-1]]))
     assert all(int(r["sp_off"][1]) == len(uv_s) for r in res)
+
+
+def test_rccl_setup_fails_on_every_rank():
+    """RcclCollective's set-up agrees across ranks: when librccl is missing
+    on one rank, every rank raises before the RCCL rendezvous (so
+    make_collective falls back on all of them together) instead of the
+    others blocking in it (gloo, 2 ranks)."""
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE="2", OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable,
+                                       os.path.join(HERE, "_rccl_consensus_worker.py")],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    for p in procs:
+        out, _ = p.communicate(timeout=120)
+        assert p.returncode == 0, out.decode()[-3000:]
+        assert b"raised" in out
+
